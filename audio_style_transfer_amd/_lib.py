@@ -1,0 +1,77 @@
+"""ctypes binding of libastyle.so (include/astyle.h).
+
+The product path has no fallback: if the in-tree library is missing or fails to load, every
+entry point raises.  Device buffers are torch tensors on the context's device; their
+``data_ptr()`` crosses the C ABI together with the current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, 'libastyle.so')
+MAX_TAPS = 32
+
+# Every symbol include/astyle.h declares (checked by tests/test_abi.py).
+EXPORTS = ('ast_create', 'ast_destroy', 'ast_workspace_bytes', 'ast_set_weight', 'ast_forward',
+           'ast_get_extract', 'ast_embeds', 'ast_content_cols', 'ast_set_targets',
+           'ast_loss_grad', 'ast_adam_step', 'ast_timing', 'ast_timing_read',
+           'ast_last_error')
+
+
+class AstCfg(ctypes.Structure):
+    _fields_ = [('batch', ctypes.c_int), ('T', ctypes.c_int),
+                ('n_cont', ctypes.c_int), ('cont_ids', ctypes.c_int * MAX_TAPS),
+                ('cnt_channels', ctypes.c_int),
+                ('n_style', ctypes.c_int), ('style_ids', ctypes.c_int * MAX_TAPS),
+                ('nb_channels', ctypes.c_int), ('gatys', ctypes.c_int),
+                ('precision', ctypes.c_int), ('lambd', ctypes.c_float)]
+
+
+class AstError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) the in-tree HIP library; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise AstError('libastyle.so not built (%s): run __graft_entry__.build() or '
+                       'python audio_style_transfer_amd/_build.py' % path)
+    lib = ctypes.CDLL(path)
+    vp, i, f, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+    fp = ctypes.POINTER(ctypes.c_float)
+    sig = {
+        'ast_create': (i, [ctypes.POINTER(AstCfg), i, ctypes.POINTER(vp)]),
+        'ast_destroy': (None, [vp]),
+        'ast_workspace_bytes': (i, [ctypes.POINTER(AstCfg), ctypes.POINTER(sz)]),
+        'ast_set_weight': (i, [vp, ctypes.c_char_p, fp, sz]),
+        'ast_forward': (i, [vp, vp, vp]),
+        'ast_get_extract': (i, [vp, i, vp, vp]),
+        'ast_embeds': (i, [vp, vp, vp, vp, vp]),
+        'ast_content_cols': (i, [vp]),
+        'ast_set_targets': (i, [vp, vp, i, vp, i]),
+        'ast_loss_grad': (i, [vp, vp, vp, vp, vp]),
+        'ast_adam_step': (i, [vp, vp, vp, vp, vp, i, f, f, f, f, vp]),
+        'ast_timing': (i, [vp, i]),
+        'ast_timing_read': (i, [vp, fp, i]),
+        'ast_last_error': (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load().ast_last_error()
+        raise AstError('libastyle error %d: %s' % (rc, msg.decode() if msg else ''))

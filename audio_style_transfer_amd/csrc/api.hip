@@ -1,0 +1,510 @@
+// C ABI of libastyle.so (declared in include/astyle.h; reference interfaces cited there).
+// Owns the per-device context: weights, activation workspace, tap bookkeeping, and the
+// launch sequence of one loss+grad evaluation (methods.py:113-137 evaluated as
+// ScipyOptimizerInterface does, methods.py:167).
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <stdio.h>
+#include <string>
+#include <vector>
+#include <algorithm>
+
+#include "../../include/astyle.h"
+#include "common.h"
+
+using namespace ast;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                     \
+    do {                                                                                 \
+        hipError_t _e = (expr);                                                          \
+        if (_e != hipSuccess)                                                            \
+            return fail(AST_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));  \
+    } while (0)
+
+constexpr int NBLK_MAX = 30;
+constexpr int NFAM = 5;   // block fwd, block bwd, gram fwd, gram bwd, other
+
+// weight offsets (floats) inside one device allocation
+constexpr size_t W0_OFF = 0;                  // [3][128]
+constexpr size_t B0_OFF = W0_OFF + 3 * C;     // [128]
+constexpr size_t BLK_OFF = B0_OFF + C;
+constexpr size_t WD = 0, WDT = 3 * C * C, BD = 6 * C * C, WR = BD + C, WRT = WR + C * C,
+                 BR = WRT + C * C, BLK_SZ = BR + C;
+constexpr size_t WB_OFF = BLK_OFF + NBLK_MAX * BLK_SZ;   // [128][16]
+constexpr size_t BB_OFF = WB_OFF + C * 16;
+constexpr size_t W_TOTAL = BB_OFF + 16;
+
+struct Occ { int ext, tensor, off, ncol; };
+
+}  // namespace
+
+struct ast_ctx {
+    ast_cfg cfg;
+    int dev = 0;
+    int nblk = 0;
+    bool need_bott = false;
+    int nu = 0, uid[32];
+    int L = 0, lmap[32];
+    std::vector<Occ> occ;
+    int ncc = 0;
+    int nchunk = 1;
+    float* cg_buf[NBLK_MAX + 1] = {};       // content grad per tensor (or null)
+    bool tensor_in_style[NBLK_MAX + 1] = {};
+    bool tensor_has_direct_content[NBLK_MAX + 1] = {};
+    // device memory
+    float* wts = nullptr;
+    float* act = nullptr; size_t tstride = 0;
+    uint32_t* mu = nullptr; uint32_t* me = nullptr;
+    float* chain[2] = {};
+    float* bott = nullptr; float* gbott = nullptr;
+    float* gpart = nullptr; float* smat = nullptr; float* spart = nullptr; float* cpart = nullptr;
+    int ncpart = 0;
+    std::vector<void*> allocs;
+    const float* phi_c = nullptr; int phi_c_shared = 0;
+    const float* phi_s = nullptr; int phi_s_shared = 0;
+    bool targets = false;
+    bool fwd_done = false;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev;
+    int ev_used = 0;
+    int timed_calls = 0;
+};
+
+namespace {
+
+int ext_to_tensor(int ext) { return ext >= 30 ? 30 : ext + 1; }
+
+int plan(const ast_cfg* c, ast_ctx* x) {
+    if (c->batch < 1 || c->T < 512 || c->T % 512)
+        return fail(AST_E_ARG, "T must be a positive multiple of 512 (masked.py:134,183)");
+    if (c->n_cont < 1 || c->n_cont > AST_MAX_TAPS || c->n_style < 1 || c->n_style > AST_MAX_TAPS)
+        return fail(AST_E_ARG, "need 1..32 content and style taps");
+    if (c->cnt_channels < 1 || c->nb_channels < 1)
+        return fail(AST_E_ARG, "cnt_channels / nb_channels must be >= 1");
+    if (c->gatys) return fail(AST_E_ARG, "gatys Gram is not built in this version");
+    if (c->precision != 0) return fail(AST_E_ARG, "only precision 0 (fp32) is built in this version");
+    int top = 0;
+    x->need_bott = false;
+    x->ncc = 0;
+    x->occ.clear();
+    for (int i = 0; i < c->n_cont; ++i) {
+        const int e = c->cont_ids[i];
+        if (e < 0 || e > 31) return fail(AST_E_ARG, "content layer ids must be in 0..31");
+        const int tns = ext_to_tensor(e);
+        top = std::max(top, tns);
+        const int width = e == 31 ? 16 : C;
+        const int ncol = std::min(c->cnt_channels, width);
+        x->occ.push_back({e, tns, x->ncc, ncol});
+        x->ncc += ncol;
+        if (e == 31) x->need_bott = true;
+        else x->tensor_has_direct_content[tns] = true;
+    }
+    x->nu = 0;
+    x->L = c->n_style;
+    for (int i = 0; i < c->n_style; ++i) {
+        const int e = c->style_ids[i];
+        if (e < 0 || e > 30)
+            return fail(AST_E_ARG, "style layer ids must be in 0..30 (extract 31 has 16 channels; "
+                                   "tf.concat with 128-channel extracts rejects it)");
+        const int tns = ext_to_tensor(e);
+        top = std::max(top, tns);
+        int u = -1;
+        for (int k = 0; k < x->nu; ++k) if (x->uid[k] == tns) u = k;
+        if (u < 0) { u = x->nu++; x->uid[u] = tns; }
+        x->lmap[i] = u;
+        x->tensor_in_style[tns] = true;
+    }
+    x->nblk = top;
+    // every dilation used must divide T (masked.py:134)
+    const int maxd = x->nblk >= 10 ? 512 : (1 << (x->nblk - 1));
+    if (c->T % maxd) return fail(AST_E_ARG, "T must be a multiple of the largest dilation");
+    // Gram time chunks: ~4096 workgroups, chunk a multiple of GT
+    int target = std::max(1, 4096 / (8 * c->batch));
+    int nch = 1;
+    while (nch * 2 <= target && (c->T / GT) % (nch * 2) == 0) nch *= 2;
+    x->nchunk = nch;
+    return 0;
+}
+
+size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
+    const size_t BTC = (size_t)c->batch * c->T * C;
+    size_t n = 0;
+    n += W_TOTAL * 4;
+    n += (size_t)(x->nblk + 1) * BTC * 4;                   // act
+    n += 2 * (size_t)x->nblk * c->batch * c->T * 16;        // mu, me
+    n += 2 * BTC * 4;                                       // chain
+    int ncg = 0;
+    for (int t = 0; t <= NBLK_MAX; ++t)
+        if (x->tensor_has_direct_content[t] || (t == 30 && x->need_bott)) ++ncg;
+    n += (size_t)ncg * BTC * 4;
+    if (x->need_bott) n += 2 * (size_t)c->batch * c->T * 16 * 4;
+    n += (size_t)c->batch * x->nchunk * C * 1024 * 4;       // gpart
+    n += (size_t)c->batch * C * 1024 * 4;                   // smat
+    n += (size_t)c->batch * C * 4;                          // spart
+    n += (size_t)c->batch * x->occ.size() * (c->T / CROWS) * 4;
+    return n;
+}
+
+int dalloc(ast_ctx* x, void** p, size_t bytes) {
+    HIPCHK(hipMalloc(p, bytes));
+    x->allocs.push_back(*p);
+    return 0;
+}
+
+hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+void tmark(ast_ctx* x, hipStream_t s) {
+    if (!x->timing || x->ev_used >= (int)x->ev.size()) return;
+    (void)hipEventRecord(x->ev[x->ev_used++], s);
+}
+
+float* blkw(ast_ctx* x, int l) { return x->wts + BLK_OFF + (size_t)l * BLK_SZ; }
+
+int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
+    const ast_cfg& c = x->cfg;
+    launch_startconv_fwd(xd, x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s);
+    if (mark) tmark(x, s);
+    for (int l = 0; l < x->nblk; ++l) {
+        FwdArgs a;
+        float* w = blkw(x, l);
+        a.ein = x->act + (size_t)l * x->tstride;
+        a.eout = x->act + (size_t)(l + 1) * x->tstride;
+        a.wd = w + WD; a.bd = w + BD; a.wr = w + WR; a.br = w + BR;
+        a.mu = x->mu + (size_t)l * c.batch * c.T * 4;
+        a.me = x->me + (size_t)l * c.batch * c.T * 4;
+        a.B = c.batch; a.T = c.T; a.d = 1 << (l % 10); a.n = c.T / a.d;
+        launch_block_fwd(a, s);
+    }
+    if (mark) tmark(x, s);
+    if (x->need_bott)
+        launch_bottleneck_fwd(x->act + (size_t)30 * x->tstride, x->bott, x->wts + WB_OFF,
+                              x->wts + BB_OFF, c.batch, c.T, s);
+    HIPCHK(hipGetLastError());
+    x->fwd_done = true;
+    return 0;
+}
+
+GramArgs gram_args(ast_ctx* x) {
+    GramArgs g;
+    memset(&g, 0, sizeof(g));
+    g.act = x->act; g.actw = x->act; g.tstride = x->tstride;
+    g.nu = x->nu;
+    for (int u = 0; u < x->nu; ++u) { g.uid[u] = x->uid[u]; g.cg[u] = x->cg_buf[x->uid[u]]; }
+    g.gpart = x->gpart; g.smat = x->smat;
+    g.B = x->cfg.batch; g.T = x->cfg.T; g.nchunk = x->nchunk;
+    return g;
+}
+
+StyleArgs style_args(ast_ctx* x) {
+    StyleArgs a;
+    memset(&a, 0, sizeof(a));
+    a.gpart = x->gpart; a.nchunk = x->nchunk;
+    a.L = x->L; a.nu = x->nu;
+    for (int i = 0; i < x->L; ++i) a.lmap[i] = x->lmap[i];
+    a.nb = std::min(x->cfg.nb_channels, C);
+    a.coef = x->cfg.lambd * 1e3f * 2.0f / (float)(a.nb * x->L * x->L);
+    a.B = x->cfg.batch;
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ast_last_error(void) { return g_err.c_str(); }
+
+int ast_workspace_bytes(const ast_cfg* cfg, size_t* out) {
+    if (!cfg || !out) return fail(AST_E_ARG, "null argument");
+    ast_ctx tmp;
+    tmp.cfg = *cfg;
+    int rc = plan(cfg, &tmp);
+    if (rc) return rc;
+    *out = workspace_bytes(cfg, &tmp);
+    return 0;
+}
+
+int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
+    if (!cfg || !out) return fail(AST_E_ARG, "null argument");
+    ast_ctx* x = new ast_ctx();
+    x->cfg = *cfg;
+    int rc = plan(cfg, x);
+    if (rc) { delete x; return rc; }
+    x->dev = hip_device;
+    hipError_t e = hipSetDevice(hip_device);
+    if (e != hipSuccess) { delete x; return fail(AST_E_HIP, hipGetErrorString(e)); }
+    const ast_cfg& c = *cfg;
+    const size_t BTC = (size_t)c.batch * c.T * C;
+    x->tstride = BTC;
+    void* p;
+#define ALLOC(dst, bytes) do { if ((rc = dalloc(x, &p, (bytes)))) { ast_destroy(x); return rc; } dst = (decltype(dst))p; } while (0)
+    ALLOC(x->wts, W_TOTAL * 4);
+    (void)hipMemset(x->wts, 0, W_TOTAL * 4);
+    ALLOC(x->act, (size_t)(x->nblk + 1) * BTC * 4);
+    ALLOC(x->mu, (size_t)x->nblk * c.batch * c.T * 16);
+    ALLOC(x->me, (size_t)x->nblk * c.batch * c.T * 16);
+    ALLOC(x->chain[0], BTC * 4);
+    ALLOC(x->chain[1], BTC * 4);
+    for (int t = 0; t <= NBLK_MAX; ++t)
+        if (x->tensor_has_direct_content[t] || (t == 30 && x->need_bott)) ALLOC(x->cg_buf[t], BTC * 4);
+    if (x->need_bott) {
+        ALLOC(x->bott, (size_t)c.batch * c.T * 16 * 4);
+        ALLOC(x->gbott, (size_t)c.batch * c.T * 16 * 4);
+    }
+    ALLOC(x->gpart, (size_t)c.batch * x->nchunk * C * 1024 * 4);
+    ALLOC(x->smat, (size_t)c.batch * C * 1024 * 4);
+    ALLOC(x->spart, (size_t)c.batch * C * 4);
+    x->ncpart = (int)x->occ.size() * (c.T / CROWS);
+    ALLOC(x->cpart, (size_t)c.batch * x->ncpart * 4);
+#undef ALLOC
+    *out = x;
+    return 0;
+}
+
+void ast_destroy(ast_ctx* x) {
+    if (!x) return;
+    (void)hipSetDevice(x->dev);
+    for (void* p : x->allocs) (void)hipFree(p);
+    for (hipEvent_t e : x->ev) (void)hipEventDestroy(e);
+    delete x;
+}
+
+int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
+    if (!x || !name || !host) return fail(AST_E_ARG, "null argument");
+    (void)hipSetDevice(x->dev);
+    std::string s(name);
+    auto put = [&](size_t off, const float* src, size_t cnt) -> int {
+        HIPCHK(hipMemcpy(x->wts + off, src, cnt * 4, hipMemcpyHostToDevice));
+        return 0;
+    };
+    auto need = [&](size_t cnt) -> int {
+        if (n != cnt) return fail(AST_E_NAME, s + ": expected " + std::to_string(cnt) + " elements");
+        return 0;
+    };
+    int rc;
+    if (s == "ae_startconv/W") { if ((rc = need(3 * C))) return rc; return put(W0_OFF, host, 3 * C); }
+    if (s == "ae_startconv/biases") { if ((rc = need(C))) return rc; return put(B0_OFF, host, C); }
+    if (s == "ae_bottleneck/W") { if ((rc = need(C * 16))) return rc; return put(WB_OFF, host, C * 16); }
+    if (s == "ae_bottleneck/biases") { if ((rc = need(16))) return rc; return put(BB_OFF, host, 16); }
+    int l = 0;
+    char tail[32];
+    if (sscanf(name, "ae_dilatedconv_%d/%31s", &l, tail) == 2 && l >= 1 && l <= NBLK_MAX) {
+        const size_t base = BLK_OFF + (size_t)(l - 1) * BLK_SZ;
+        if (!strcmp(tail, "W")) {
+            if ((rc = need(3 * C * C))) return rc;
+            std::vector<float> tr(3 * C * C);
+            for (int k = 0; k < 3; ++k)
+                for (int ci = 0; ci < C; ++ci)
+                    for (int co = 0; co < C; ++co)
+                        tr[(size_t)k * C * C + co * C + ci] = host[(size_t)k * C * C + ci * C + co];
+            if ((rc = put(base + WD, host, 3 * C * C))) return rc;
+            return put(base + WDT, tr.data(), 3 * C * C);
+        }
+        if (!strcmp(tail, "biases")) { if ((rc = need(C))) return rc; return put(base + BD, host, C); }
+    }
+    if (sscanf(name, "ae_res_%d/%31s", &l, tail) == 2 && l >= 1 && l <= NBLK_MAX) {
+        const size_t base = BLK_OFF + (size_t)(l - 1) * BLK_SZ;
+        if (!strcmp(tail, "W")) {
+            if ((rc = need(C * C))) return rc;
+            std::vector<float> tr(C * C);
+            for (int ci = 0; ci < C; ++ci)
+                for (int co = 0; co < C; ++co) tr[co * C + ci] = host[ci * C + co];
+            if ((rc = put(base + WR, host, C * C))) return rc;
+            return put(base + WRT, tr.data(), C * C);
+        }
+        if (!strcmp(tail, "biases")) { if ((rc = need(C))) return rc; return put(base + BR, host, C); }
+    }
+    return fail(AST_E_NAME, "not an encoder variable: " + s);
+}
+
+int ast_forward(ast_ctx* x, const float* xd, void* stream) {
+    if (!x || !xd) return fail(AST_E_ARG, "null argument");
+    return run_forward(x, xd, S(stream));
+}
+
+int ast_get_extract(ast_ctx* x, int ext, float* out, void* stream) {
+    if (!x || !out) return fail(AST_E_ARG, "null argument");
+    if (!x->fwd_done) return fail(AST_E_STATE, "ast_forward has not run");
+    const ast_cfg& c = x->cfg;
+    if (ext == 31) {
+        if (!x->need_bott) return fail(AST_E_ARG, "extract 31 (bottleneck) is not computed for these taps");
+        HIPCHK(hipMemcpyAsync(out, x->bott, (size_t)c.batch * c.T * 16 * 4, hipMemcpyDeviceToDevice, S(stream)));
+        return 0;
+    }
+    if (ext < 0 || ext > 30) return fail(AST_E_ARG, "extract id out of range");
+    const int tns = ext_to_tensor(ext);
+    if (tns > x->nblk) return fail(AST_E_ARG, "extract beyond the blocks this context runs");
+    HIPCHK(hipMemcpyAsync(out, x->act + (size_t)tns * x->tstride, x->tstride * 4,
+                          hipMemcpyDeviceToDevice, S(stream)));
+    return 0;
+}
+
+int ast_content_cols(ast_ctx* x) { return x ? x->ncc : 0; }
+
+int ast_embeds(ast_ctx* x, const float* xd, float* emb_c, float* emb_s, void* stream) {
+    if (!x || !xd) return fail(AST_E_ARG, "null argument");
+    hipStream_t s = S(stream);
+    int rc = run_forward(x, xd, s);
+    if (rc) return rc;
+    const ast_cfg& c = x->cfg;
+    if (emb_c) {
+        for (const Occ& o : x->occ) {
+            ContentArgs a;
+            memset(&a, 0, sizeof(a));
+            a.e = o.ext == 31 ? x->bott : x->act + (size_t)o.tensor * x->tstride;
+            a.W = o.ext == 31 ? 16 : C;
+            a.ncc = x->ncc; a.off = o.off; a.ncol = o.ncol;
+            a.embc = emb_c; a.B = c.batch; a.T = c.T;
+            launch_content(a, s);
+        }
+    }
+    if (emb_s) {
+        GramArgs g = gram_args(x);
+        launch_gram_fwd(g, s);
+        StyleArgs a = style_args(x);
+        a.embs = emb_s;
+        launch_style_ours(a, s);
+    }
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int ast_set_targets(ast_ctx* x, const float* phi_c, int phi_c_shared, const float* phi_s,
+                    int phi_s_shared) {
+    if (!x || !phi_c || !phi_s) return fail(AST_E_ARG, "null argument");
+    x->phi_c = phi_c; x->phi_c_shared = phi_c_shared;
+    x->phi_s = phi_s; x->phi_s_shared = phi_s_shared;
+    x->targets = true;
+    return 0;
+}
+
+int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* stream) {
+    if (!x || !xd || !grad || !parts) return fail(AST_E_ARG, "null argument");
+    if (!x->targets) return fail(AST_E_STATE, "ast_set_targets has not been called");
+    (void)hipSetDevice(x->dev);
+    hipStream_t s = S(stream);
+    const ast_cfg& c = x->cfg;
+    tmark(x, s);
+    int rc = run_forward(x, xd, s, true);
+    if (rc) return rc;
+    // content taps (methods.py:58, 116-117)
+    const float ccoef = 10.0f * 2.0f / ((float)c.T * (float)x->ncc);
+    const int tiles = c.T / CROWS;
+    bool first_cg[NBLK_MAX + 1];
+    for (int t = 0; t <= NBLK_MAX; ++t) first_cg[t] = true;
+    bool first_bott = true;
+    for (size_t i = 0; i < x->occ.size(); ++i) {
+        const Occ& o = x->occ[i];
+        ContentArgs a;
+        memset(&a, 0, sizeof(a));
+        a.W = o.ext == 31 ? 16 : C;
+        a.e = o.ext == 31 ? x->bott : x->act + (size_t)o.tensor * x->tstride;
+        a.phi = x->phi_c; a.phi_bstride = x->phi_c_shared ? 0 : (size_t)c.T * x->ncc;
+        a.ncc = x->ncc; a.off = o.off; a.ncol = o.ncol; a.coef = ccoef;
+        if (o.ext == 31) { a.cg = x->gbott; a.accumulate = !first_bott; first_bott = false; }
+        else { a.cg = x->cg_buf[o.tensor]; a.accumulate = !first_cg[o.tensor]; first_cg[o.tensor] = false; }
+        a.lpart = x->cpart + i * tiles; a.lstride = (size_t)x->ncpart;
+        a.B = c.batch; a.T = c.T;
+        launch_content(a, s);
+    }
+    if (x->need_bott)
+        launch_bottleneck_bwd(x->gbott, x->cg_buf[30], x->wts + WB_OFF, !first_cg[30], c.batch, c.T, s);
+    // style (methods.py:62-76, 118-119)
+    GramArgs g = gram_args(x);
+    tmark(x, s);
+    launch_gram_fwd(g, s);
+    tmark(x, s);
+    StyleArgs sa = style_args(x);
+    sa.phi = x->phi_s;
+    sa.phi_bstride = x->phi_s_shared ? 0 : (size_t)sa.nb * x->L * x->L;
+    sa.smat = x->smat; sa.spart = x->spart;
+    launch_style_ours(sa, s);
+    tmark(x, s);
+    launch_gram_bwd(g, s);
+    tmark(x, s);
+    // backward chain through the blocks
+    for (int l = x->nblk - 1; l >= 0; --l) {
+        BwdArgs a;
+        float* w = blkw(x, l);
+        const int tin = l + 1;
+        a.gin = (l == x->nblk - 1) ? nullptr : x->chain[(l + 1) & 1];
+        a.din = x->tensor_in_style[tin] ? x->act + (size_t)tin * x->tstride : x->cg_buf[tin];
+        a.gout = x->chain[l & 1];
+        a.wr = w + WR; a.wrT = w + WRT; a.wdT = w + WDT;
+        a.mu = x->mu + (size_t)l * c.batch * c.T * 4;
+        a.me = x->me + (size_t)l * c.batch * c.T * 4;
+        a.B = c.batch; a.T = c.T; a.d = 1 << (l % 10); a.n = c.T / a.d;
+        launch_block_bwd(a, s);
+    }
+    tmark(x, s);
+    launch_startconv_bwd(x->chain[0], grad, x->wts + W0_OFF, c.batch, c.T, s);
+    const int nb = std::min(c.nb_channels, C);
+    launch_finalize(parts, x->cpart, x->ncpart, 10.0f / ((float)c.T * (float)x->ncc), x->spart, C,
+                    1e3f / (float)(nb * x->L * x->L), c.lambd, c.batch, s);
+    tmark(x, s);
+    HIPCHK(hipGetLastError());
+    if (x->timing && x->ev_used <= (int)x->ev.size()) x->timed_calls++;
+    x->fwd_done = false;   // tapped tensors now hold their gradients, not activations
+    return 0;
+}
+
+int ast_adam_step(ast_ctx* x, float* xd, float* m, float* v, const float* grad, int step,
+                  float lr, float b1, float b2, float eps, void* stream) {
+    if (!x || !xd || !m || !v || !grad || step < 1) return fail(AST_E_ARG, "bad argument");
+    const float bc1 = 1.0f - powf(b1, (float)step), bc2 = 1.0f - powf(b2, (float)step);
+    launch_adam(xd, m, v, grad, (size_t)x->cfg.batch * x->cfg.T, lr, b1, b2, eps, bc1, bc2, S(stream));
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// Event layout per timed ast_loss_grad call (8 marks):
+//  m0 start | startconv | m1 | blocks fwd | m2 | content | m3 gram fwd m4 style m5 gram bwd m6
+//  | blocks bwd | m7 | startconv bwd + finalize | m8
+int ast_timing(ast_ctx* x, int enable) {
+    if (!x) return fail(AST_E_ARG, "null argument");
+    (void)hipSetDevice(x->dev);
+    if (enable) {
+        if (x->ev.empty()) {
+            x->ev.resize(9 * 512);
+            for (auto& e : x->ev) HIPCHK(hipEventCreate(&e));
+        }
+        x->ev_used = 0;
+        x->timed_calls = 0;
+    }
+    x->timing = enable != 0;
+    return 0;
+}
+
+int ast_timing_read(ast_ctx* x, float* out, int n) {
+    if (!x || !out) return fail(AST_E_ARG, "null argument");
+    float fam[NFAM] = {0, 0, 0, 0, 0};
+    const int per = 9;
+    const int calls = std::min(x->timed_calls, x->ev_used / per);
+    for (int k = 0; k < calls; ++k) {
+        hipEvent_t* e = &x->ev[(size_t)k * per];
+        float t[8];
+        for (int i = 0; i < 8; ++i) {
+            HIPCHK(hipEventSynchronize(e[i + 1]));
+            HIPCHK(hipEventElapsedTime(&t[i], e[i], e[i + 1]));
+        }
+        fam[0] += t[1];                  // blocks fwd
+        fam[1] += t[6];                  // blocks bwd
+        fam[2] += t[3];                  // gram fwd
+        fam[3] += t[5];                  // gram bwd
+        fam[4] += t[0] + t[2] + t[4] + t[7];
+    }
+    float vals[7] = {fam[0], fam[1], fam[2], fam[3], fam[4], (float)calls, (float)x->nblk};
+    for (int i = 0; i < n && i < 7; ++i) out[i] = vals[i];
+    return 0;
+}
+
+}  // extern "C"

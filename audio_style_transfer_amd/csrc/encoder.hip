@@ -1,0 +1,336 @@
+// NSynth WaveNet encoder (model.py:80-127) forward and backward-to-input on gfx950.
+//
+// One fused kernel per residual block and direction:
+//   fwd  e_{l+1} = e_l + Wr^T relu(b_d + sum_k Wd[k]^T relu(e_l)[p+k-1]) + b_r
+//        (model.py:99-114; masked.py:110-160 with causal=False -> symmetric taps)
+//   bwd  g_l = tot + [e_l>0] * sum_k Wd[k] ([u>0] * (Wr tot))[p-k+1],  tot = g_{l+1} + D_{l+1}
+// A workgroup owns TM positions of one clip in time_to_batch order (common.h), stages the
+// TM+2 input rows in LDS once, and runs both GEMMs (K = 3*128 then 128) on
+// v_mfma_f32_32x32x2_f32 with fp32 accumulation; the bias/relu/residual/mask epilogues are
+// fused and the relu masks leave as bits (16 B per row) for the backward.
+#include "common.h"
+
+namespace ast {
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// acc[nt] += A[k] * B[k][colb + 32 nt] for k in [0,128): A from an LDS row (this lane's
+// M-row), B (row-major [k][C]) from global/L2.  Lane half h feeds k = 4ps + 2h (+1).
+template <bool RELU>
+__device__ __forceinline__ void mm_k128(f32x16 (&acc)[2], const float* __restrict__ arow,
+                                        bool valid, const float* __restrict__ Bm, int colb,
+                                        int h) {
+#pragma unroll 8
+    for (int ps = 0; ps < 32; ++ps) {
+        const int k0 = 4 * ps + 2 * h;
+        const float2 av = *reinterpret_cast<const float2*>(arow + k0);
+        float a0 = av.x, a1 = av.y;
+        if (RELU) { a0 = fmaxf(a0, 0.f); a1 = fmaxf(a1, 0.f); }
+        a0 = valid ? a0 : 0.f;
+        a1 = valid ? a1 : 0.f;
+        const float* b0 = Bm + (size_t)k0 * C + colb;
+        const float b00 = b0[0], b01 = b0[32], b10 = b0[C], b11 = b0[C + 32];
+        acc[0] = mfma32(a0, b00, acc[0]);
+        acc[1] = mfma32(a0, b01, acc[1]);
+        acc[0] = mfma32(a1, b10, acc[0]);
+        acc[1] = mfma32(a1, b11, acc[1]);
+    }
+}
+
+__device__ __forceinline__ int pos_to_t(int p, int n, int d) { return (p % n) * d + p / n; }
+
+__global__ void __launch_bounds__(256) k_block_fwd(FwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float X[(TM + 2) * XS];
+    __shared__ __attribute__((aligned(16))) float V[TM * XS];
+    __shared__ __attribute__((aligned(16))) uint32_t MB[TM * 4];
+    __shared__ int TT[TM + 2];
+    const int tiles = a.T / TM;
+    const int b = blockIdx.x / tiles;
+    const int p0 = (blockIdx.x - b * tiles) * TM;
+    const size_t cb = (size_t)b * a.T * C;
+    const size_t mbase = (size_t)b * a.T * 4;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+
+    if (tid < TM + 2) {
+        const int p = p0 - 1 + tid;
+        TT[tid] = (p >= 0 && p < a.T) ? pos_to_t(p, a.n, a.d) : -1;
+    }
+    __syncthreads();
+    for (int i = tid; i < (TM + 2) * 32; i += 256) {
+        const int rr = i >> 5, q = i & 31;
+        const int t = TT[rr];
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (t >= 0) v = *reinterpret_cast<const float4*>(a.ein + cb + (size_t)t * C + q * 4);
+        float2* dst = reinterpret_cast<float2*>(&X[rr * XS + q * 4]);
+        dst[0] = make_float2(v.x, v.y);
+        dst[1] = make_float2(v.z, v.w);
+    }
+    __syncthreads();
+
+    // e_l > 0 bits of the tile rows (consumed by the backward's relu(e_l) mask)
+    for (int rr = w; rr < TM; rr += 4) {
+        const float v0 = X[(rr + 1) * XS + lane], v1 = X[(rr + 1) * XS + 64 + lane];
+        const unsigned long long q0 = __ballot(v0 > 0.f), q1 = __ballot(v1 > 0.f);
+        if (lane == 0)
+            *reinterpret_cast<uint4*>(a.me + mbase + (size_t)TT[rr + 1] * 4) =
+                make_uint4((uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32));
+    }
+
+    const int wm = w & 1, wn = w >> 1, r = lane & 31, h = lane >> 5;
+    const int row = wm * 32 + r;
+    const int m = (p0 + row) % a.n;
+    const bool ok0 = m > 0, ok2 = m < a.n - 1;
+    const int colb = wn * 64 + r;
+
+    // GEMM 1: dilated conv, K = 3 taps x 128 (masked.py:154)
+    f32x16 acc[2];
+    for (int i = 0; i < 16; ++i) { acc[0][i] = 0.f; acc[1][i] = 0.f; }
+    mm_k128<true>(acc, &X[(row + 0) * XS], ok0, a.wd + 0 * C * C, colb, h);
+    mm_k128<true>(acc, &X[(row + 1) * XS], true, a.wd + 1 * C * C, colb, h);
+    mm_k128<true>(acc, &X[(row + 2) * XS], ok2, a.wd + 2 * C * C, colb, h);
+
+    {   // epilogue 1: bias (masked.py:155), relu (model.py:107), mask bits
+        const float bd0 = a.bd[colb], bd1 = a.bd[colb + 32];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int R0 = wm * 32 + (i & 3) + 8 * (i >> 2);
+            const int R = R0 + 4 * h;
+            const float u0 = acc[0][i] + bd0, u1 = acc[1][i] + bd1;
+            const unsigned long long q0 = __ballot(u0 > 0.f), q1 = __ballot(u1 > 0.f);
+            V[R * XS + colb] = fmaxf(u0, 0.f);
+            V[R * XS + colb + 32] = fmaxf(u1, 0.f);
+            if (lane == 0) {
+                MB[R0 * 4 + wn * 2 + 0] = (uint32_t)q0;
+                MB[R0 * 4 + wn * 2 + 1] = (uint32_t)q1;
+                MB[(R0 + 4) * 4 + wn * 2 + 0] = (uint32_t)(q0 >> 32);
+                MB[(R0 + 4) * 4 + wn * 2 + 1] = (uint32_t)(q1 >> 32);
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < TM)
+        *reinterpret_cast<uint4*>(a.mu + mbase + (size_t)TT[tid + 1] * 4) =
+            *reinterpret_cast<const uint4*>(&MB[tid * 4]);
+
+    // GEMM 2: 1x1 residual projection (model.py:109-114)
+    for (int i = 0; i < 16; ++i) { acc[0][i] = 0.f; acc[1][i] = 0.f; }
+    mm_k128<false>(acc, &V[row * XS], true, a.wr, colb, h);
+    const float br0 = a.br[colb], br1 = a.br[colb + 32];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int R = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const size_t o = cb + (size_t)TT[R + 1] * C + colb;
+        a.eout[o] = X[(R + 1) * XS + colb] + (acc[0][i] + br0);
+        a.eout[o + 32] = X[(R + 1) * XS + colb + 32] + (acc[1][i] + br1);
+    }
+}
+
+__device__ __forceinline__ float bitf(uint32_t word, int bit) {
+    return ((word >> bit) & 1u) ? 1.f : 0.f;
+}
+
+__global__ void __launch_bounds__(256) k_block_bwd(BwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float G[(TM + 2) * XS];
+    __shared__ __attribute__((aligned(16))) float U[(TM + 2) * XS];
+    __shared__ __attribute__((aligned(16))) uint32_t MU[(TM + 2) * 4];
+    __shared__ __attribute__((aligned(16))) uint32_t ME[TM * 4];
+    __shared__ int TT[TM + 2];
+    const int tiles = a.T / TM;
+    const int b = blockIdx.x / tiles;
+    const int p0 = (blockIdx.x - b * tiles) * TM;
+    const size_t cb = (size_t)b * a.T * C;
+    const size_t mbase = (size_t)b * a.T * 4;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+
+    if (tid < TM + 2) {
+        const int p = p0 - 1 + tid;
+        TT[tid] = (p >= 0 && p < a.T) ? pos_to_t(p, a.n, a.d) : -1;
+    }
+    __syncthreads();
+    for (int i = tid; i < (TM + 2) * 32; i += 256) {
+        const int rr = i >> 5, q = i & 31;
+        const int t = TT[rr];
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (t >= 0) {
+            const size_t o = cb + (size_t)t * C + q * 4;
+            if (a.gin) v = *reinterpret_cast<const float4*>(a.gin + o);
+            if (a.din) {
+                const float4 d4 = *reinterpret_cast<const float4*>(a.din + o);
+                v.x += d4.x; v.y += d4.y; v.z += d4.z; v.w += d4.w;
+            }
+        }
+        float2* dst = reinterpret_cast<float2*>(&G[rr * XS + q * 4]);
+        dst[0] = make_float2(v.x, v.y);
+        dst[1] = make_float2(v.z, v.w);
+    }
+    if (tid < TM + 2) {
+        const int t = TT[tid];
+        uint4 mw = make_uint4(0, 0, 0, 0);
+        if (t >= 0) mw = *reinterpret_cast<const uint4*>(a.mu + mbase + (size_t)t * 4);
+        *reinterpret_cast<uint4*>(&MU[tid * 4]) = mw;
+        if (tid < TM)
+            *reinterpret_cast<uint4*>(&ME[tid * 4]) =
+                *reinterpret_cast<const uint4*>(a.me + mbase + (size_t)TT[tid + 1] * 4);
+    }
+    __syncthreads();
+
+    const int wm = w & 1, wn = w >> 1, r = lane & 31, h = lane >> 5;
+    const int row = wm * 32 + r;
+    const int m = (p0 + row) % a.n;
+    const bool ok0 = m > 0, ok2 = m < a.n - 1;
+    const int colb = wn * 64 + r;
+
+    // step 1: g_u = [u>0] * (Wr tot) for the tile rows (MFMA) ...
+    f32x16 acc[2];
+    for (int i = 0; i < 16; ++i) { acc[0][i] = 0.f; acc[1][i] = 0.f; }
+    mm_k128<false>(acc, &G[(row + 1) * XS], true, a.wrT, colb, h);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int R = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        U[(R + 1) * XS + colb] = acc[0][i] * bitf(MU[(R + 1) * 4 + wn * 2 + 0], r);
+        U[(R + 1) * XS + colb + 32] = acc[1][i] * bitf(MU[(R + 1) * 4 + wn * 2 + 1], r);
+    }
+    // ... and for the two halo rows (VALU; they feed the neighbour taps only)
+    {
+        const int hr = tid >> 7, i = tid & 127;
+        const int rr = hr ? TM + 1 : 0;
+        float s = 0.f;
+        if (TT[rr] >= 0) {
+            const float* wrow = a.wr + (size_t)i * C;
+            const float* grow = &G[rr * XS];
+#pragma unroll 8
+            for (int o = 0; o < C; ++o) s = fmaf(grow[o], wrow[o], s);
+            s *= bitf(MU[rr * 4 + (i >> 5)], i & 31);
+        }
+        U[rr * XS + i] = s;
+    }
+    __syncthreads();
+
+    // step 2: gh = sum_k Wd[k] g_u[p-k+1]  (transposed dilated conv)
+    for (int i = 0; i < 16; ++i) { acc[0][i] = 0.f; acc[1][i] = 0.f; }
+    mm_k128<false>(acc, &U[(row + 2) * XS], ok2, a.wdT + 0 * C * C, colb, h);
+    mm_k128<false>(acc, &U[(row + 1) * XS], true, a.wdT + 1 * C * C, colb, h);
+    mm_k128<false>(acc, &U[(row + 0) * XS], ok0, a.wdT + 2 * C * C, colb, h);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int R = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const size_t o = cb + (size_t)TT[R + 1] * C + colb;
+        a.gout[o] = G[(R + 1) * XS + colb] + bitf(ME[R * 4 + wn * 2 + 0], r) * acc[0][i];
+        a.gout[o + 32] = G[(R + 1) * XS + colb + 32] + bitf(ME[R * 4 + wn * 2 + 1], r) * acc[1][i];
+    }
+}
+
+// ae_startconv (model.py:88-93): 1 -> 128 channels, K=3, d=1, input x/128 (model.py:82).
+__global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__ x,
+                                                       float* __restrict__ e0,
+                                                       const float* __restrict__ w0,
+                                                       const float* __restrict__ b0, int B,
+                                                       int T) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;   // (row, float4)
+    const size_t rowi = i >> 5;
+    if (rowi >= (size_t)B * T) return;
+    const int q = (int)(i & 31);
+    const int t = (int)(rowi % T);
+    const float* xr = x + (rowi - t);
+    const float xm = t > 0 ? xr[t - 1] / 128.0f : 0.f;
+    const float x0 = xr[t] / 128.0f;
+    const float xp = t < T - 1 ? xr[t + 1] / 128.0f : 0.f;
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = q * 4 + j;
+        o[j] = (w0[c] * xm + w0[C + c] * x0 + w0[2 * C + c] * xp) + b0[c];
+    }
+    *reinterpret_cast<float4*>(e0 + rowi * C + q * 4) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
+// d loss / d x = (1/128) sum_k sum_c W0[k][c] g0[t-k+1][c]; one wave per sample.
+__global__ void __launch_bounds__(256) k_startconv_bwd(const float* __restrict__ g0,
+                                                       float* __restrict__ gx,
+                                                       const float* __restrict__ w0, int B,
+                                                       int T) {
+    const size_t wid = ((size_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wid >= (size_t)B * T) return;
+    const int t = (int)(wid % T);
+    const float* base = g0 + (wid - t) * C;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int tt = t - k + 1;
+        if (tt < 0 || tt >= T) continue;
+        const float2 gv = *reinterpret_cast<const float2*>(base + (size_t)tt * C + 2 * lane);
+        s = fmaf(w0[k * C + 2 * lane], gv.x, s);
+        s = fmaf(w0[k * C + 2 * lane + 1], gv.y, s);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) gx[wid] = s / 128.0f;
+}
+
+// ae_bottleneck (model.py:121-127): 1x1, 128 -> 16.  Thread per (row, out channel).
+__global__ void __launch_bounds__(256) k_bottleneck_fwd(const float* __restrict__ e,
+                                                        float* __restrict__ y,
+                                                        const float* __restrict__ wb,
+                                                        const float* __restrict__ bb, int B,
+                                                        int T) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)B * T * 16) return;
+    const size_t rowi = i >> 4;
+    const int j = (int)(i & 15);
+    const float* er = e + rowi * C;
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s = fmaf(er[c], wb[c * 16 + j], s);
+    y[i] = s + bb[j];
+}
+
+// ge[row][c] (+)= sum_j Wb[c][j] gy[row][j]
+__global__ void __launch_bounds__(256) k_bottleneck_bwd(const float* __restrict__ gy,
+                                                        float* __restrict__ ge,
+                                                        const float* __restrict__ wb,
+                                                        int accumulate, int B, int T) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)B * T * C) return;
+    const size_t rowi = i >> 7;
+    const int c = (int)(i & 127);
+    const float* g = gy + rowi * 16;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s = fmaf(wb[c * 16 + j], g[j], s);
+    ge[i] = accumulate ? ge[i] + s : s;
+}
+
+void launch_block_fwd(const FwdArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_block_fwd, dim3(a.B * (a.T / TM)), dim3(256), 0, s, a);
+}
+void launch_block_bwd(const BwdArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_block_bwd, dim3(a.B * (a.T / TM)), dim3(256), 0, s, a);
+}
+void launch_startconv_fwd(const float* x, float* e0, const float* w0, const float* b0, int B,
+                          int T, hipStream_t s) {
+    const size_t n = (size_t)B * T * 32;
+    hipLaunchKernelGGL(k_startconv_fwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x,
+                       e0, w0, b0, B, T);
+}
+void launch_startconv_bwd(const float* g0, float* gx, const float* w0, int B, int T,
+                          hipStream_t s) {
+    const size_t n = (size_t)B * T * 64;
+    hipLaunchKernelGGL(k_startconv_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g0,
+                       gx, w0, B, T);
+}
+void launch_bottleneck_fwd(const float* e, float* y, const float* wb, const float* bb, int B,
+                           int T, hipStream_t s) {
+    const size_t n = (size_t)B * T * 16;
+    hipLaunchKernelGGL(k_bottleneck_fwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, e,
+                       y, wb, bb, B, T);
+}
+void launch_bottleneck_bwd(const float* gy, float* ge, const float* wb, int accumulate, int B,
+                           int T, hipStream_t s) {
+    const size_t n = (size_t)B * T * C;
+    hipLaunchKernelGGL(k_bottleneck_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       gy, ge, wb, accumulate, B, T);
+}
+
+}  // namespace ast

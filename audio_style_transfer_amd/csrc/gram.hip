@@ -1,0 +1,317 @@
+// Channel-wise ("ours") Gram, l2-normalise, style/content losses and their gradients
+// (methods.py:58-76, 113-125) on gfx950.
+//
+// Gram fwd: G_c[u][u'] = sum_t E_u[t][c] E_u'[t][c] for the U unique tapped tensors, one
+//   v_mfma_f32_32x32x2_f32 per (channel, 2 time steps) with A = B = the same register
+//   (lane (i,h) holds E_i[t0+2s+h][c]); partial sums per time chunk, no atomics.
+// Gram bwd: D_u[t][c] = sum_u' S~_c[u][u'] E_u'[t][c] (+ content grad), S~ = dG + dG^T folded
+//   onto unique tensors; written in place over E_u (E is dead after this pass: the backward
+//   chain uses the mask bits).
+// Both stage a [32 tensors][32 t][16 ch] fp32 tile in LDS (layer stride 545, row stride 17:
+// both the row-indexed and the column-indexed operand reads are bank-conflict free).
+#include "common.h"
+
+namespace ast {
+
+__device__ __forceinline__ f32x16 mfma32g(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void gram_stage(float* Et, const GramArgs& a, int b, int t0, int c0,
+                                           int tid) {
+    for (int i = tid; i < a.nu * GT * 4; i += 256) {
+        const int u = i / (GT * 4), rem = i - u * (GT * 4);
+        const int tt = rem >> 2, q = rem & 3;
+        const float4 v = *reinterpret_cast<const float4*>(
+            a.act + (size_t)a.uid[u] * a.tstride + ((size_t)b * a.T + t0 + tt) * C + c0 + q * 4);
+        float* dst = &Et[u * GLS + tt * GRS + q * 4];
+        dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_gram_fwd(GramArgs a) {
+    __shared__ float Et[32 * GLS];
+    const int ncg = C / GCH;
+    int bid = blockIdx.x;
+    const int cgi = bid % ncg; bid /= ncg;
+    const int ch = bid % a.nchunk;
+    const int b = bid / a.nchunk;
+    const int c0 = cgi * GCH;
+    const int tlen = a.T / a.nchunk, tbeg = ch * tlen;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    for (int i = a.nu * GLS + tid; i < 32 * GLS; i += 256) Et[i] = 0.f;
+
+    f32x16 acc[4];
+    for (int cc = 0; cc < 4; ++cc)
+        for (int i = 0; i < 16; ++i) acc[cc][i] = 0.f;
+    for (int t0 = tbeg; t0 < tbeg + tlen; t0 += GT) {
+        __syncthreads();
+        gram_stage(Et, a, b, t0, c0, tid);
+        __syncthreads();
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const int c = w * 4 + cc;
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                const float v = Et[r * GLS + (2 * s + h) * GRS + c];
+                acc[cc] = mfma32g(v, v, acc[cc]);
+            }
+        }
+    }
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+        float* dst = a.gpart + (((size_t)b * a.nchunk + ch) * C + c0 + w * 4 + cc) * 1024;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int R = (i & 3) + 8 * (i >> 2) + 4 * h;
+            dst[R * 32 + r] = acc[cc][i];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_gram_bwd(GramArgs a) {
+    __shared__ float Et[32 * GLS];
+    const int ncg = C / GCH;
+    int bid = blockIdx.x;
+    const int cgi = bid % ncg; bid /= ncg;
+    const int ch = bid % a.nchunk;
+    const int b = bid / a.nchunk;
+    const int c0 = cgi * GCH;
+    const int tlen = a.T / a.nchunk, tbeg = ch * tlen;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    for (int i = a.nu * GLS + tid; i < 32 * GLS; i += 256) Et[i] = 0.f;
+
+    // A fragments: S~_c[i = r][k = 2s + h] for this wave's 4 channels
+    float sa[4][16];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+        const float* sm = a.smat + ((size_t)b * C + c0 + w * 4 + cc) * 1024 + r * 32 + h;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) sa[cc][s] = sm[2 * s];
+    }
+    for (int t0 = tbeg; t0 < tbeg + tlen; t0 += GT) {
+        __syncthreads();
+        gram_stage(Et, a, b, t0, c0, tid);
+        __syncthreads();
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const int c = w * 4 + cc;
+            f32x16 acc;
+            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+                acc = mfma32g(sa[cc][s], Et[(2 * s + h) * GLS + r * GRS + c], acc);
+            // this wave alone reads/writes column c: overwrite E with D in place
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int R = (i & 3) + 8 * (i >> 2) + 4 * h;
+                Et[R * GLS + r * GRS + c] = acc[i];
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < a.nu * GT * 4; i += 256) {
+            const int u = i / (GT * 4), rem = i - u * (GT * 4);
+            const int tt = rem >> 2, q = rem & 3;
+            const size_t o = (size_t)a.uid[u] * a.tstride + ((size_t)b * a.T + t0 + tt) * C + c0 + q * 4;
+            const float* src = &Et[u * GLS + tt * GRS + q * 4];
+            float4 v = make_float4(src[0], src[1], src[2], src[3]);
+            const float* cgp = a.cg[u];
+            if (cgp) {
+                const float4 g = *reinterpret_cast<const float4*>(
+                    cgp + ((size_t)b * a.T + t0 + tt) * C + c0 + q * 4);
+                v.x += g.x; v.y += g.y; v.z += g.z; v.w += g.w;
+            }
+            *reinterpret_cast<float4*>(a.actw + o) = v;
+        }
+    }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// One wave per (clip, channel): sum chunk partials, expand unique -> list, l2-normalise
+// (methods.py:74), style loss vs phi (methods.py:118-119), d loss / d G, fold S = dG + dG^T
+// back onto unique tensors.
+__global__ void __launch_bounds__(256) k_style_ours(StyleArgs a) {
+    __shared__ float Gu[4][32 * 33];
+    __shared__ float dG[4][32 * 33];
+    __shared__ float St[4][32 * 32];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int b = blockIdx.x / (C / 4);
+    const int c = (blockIdx.x % (C / 4)) * 4 + w;
+    const int L = a.L;
+    for (int e = lane; e < 1024; e += 64) {
+        float s = 0.f;
+        for (int ch = 0; ch < a.nchunk; ++ch)
+            s += a.gpart[(((size_t)b * a.nchunk + ch) * C + c) * 1024 + e];
+        Gu[w][(e >> 5) * 33 + (e & 31)] = s;
+        St[w][e] = 0.f;
+    }
+    __syncthreads();
+    float g[16];
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int e = lane + 64 * k;
+        g[k] = 0.f;
+        if (e < L * L) {
+            const int l = e / L, l2 = e - l * L;
+            g[k] = Gu[w][a.lmap[l] * 33 + a.lmap[l2]];
+        }
+        ss = fmaf(g[k], g[k], ss);
+    }
+    ss = wave_sum(ss);
+    const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+    const bool active = c < a.nb;
+    const float* phi = a.phi ? a.phi + (size_t)b * a.phi_bstride + (size_t)c * L * L : nullptr;
+    float sd = 0.f, dot = 0.f;
+    float dgn[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int e = lane + 64 * k;
+        dgn[k] = 0.f;
+        if (e < L * L && active) {
+            const float gn = g[k] * inv;
+            if (a.embs) a.embs[(((size_t)b * a.nb) + c) * L * L + e] = gn;
+            if (a.phi) {
+                const float diff = gn - phi[e];
+                sd = fmaf(diff, diff, sd);
+                dgn[k] = a.coef * diff;
+                dot = fmaf(gn, dgn[k], dot);
+            }
+        }
+    }
+    sd = wave_sum(sd);
+    dot = wave_sum(dot);
+    const float big = ss >= 1e-12f ? 1.f : 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int e = lane + 64 * k;
+        if (e < L * L) {
+            const int l = e / L, l2 = e - l * L;
+            dG[w][l * 33 + l2] = dgn[k] * inv - big * (g[k] * inv) * dot * inv;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int e = lane + 64 * k;
+        if (e < L * L) {
+            const int l = e / L, l2 = e - l * L;
+            const float sv = dG[w][l * 33 + l2] + dG[w][l2 * 33 + l];
+            atomicAdd(&St[w][a.lmap[l] * 32 + a.lmap[l2]], sv);
+        }
+    }
+    __syncthreads();
+    if (a.smat) {
+        float* dst = a.smat + ((size_t)b * C + c) * 1024;
+        for (int e = lane; e < 1024; e += 64) dst[e] = St[w][e];
+    }
+    if (lane == 0 && a.spart) a.spart[(size_t)b * C + c] = sd;
+}
+
+// Content taps (methods.py:58,116-117): cg = coef * (E[..., :ncol] - phi[..., off:off+ncol]),
+// partial sums of the squared error per CROWS rows.  Optionally copies the tap into emb.
+__global__ void __launch_bounds__(256) k_content(ContentArgs a) {
+    __shared__ float red[4];
+    const int tilesPer = a.T / CROWS;
+    const int b = blockIdx.x / tilesPer;
+    const int t0 = (blockIdx.x - b * tilesPer) * CROWS;
+    const int tid = threadIdx.x;
+    float sd = 0.f;
+    for (int i = tid; i < CROWS * a.W; i += 256) {
+        const int tt = i / a.W, c = i - tt * a.W;
+        const size_t row = (size_t)b * a.T + t0 + tt;
+        const float e = a.e[row * a.W + c];
+        float d = 0.f;
+        if (c < a.ncol) {
+            if (a.embc) a.embc[row * a.ncc + a.off + c] = e;
+            if (a.phi) {
+                d = e - a.phi[(size_t)b * a.phi_bstride + (size_t)(t0 + tt) * a.ncc + a.off + c];
+                sd = fmaf(d, d, sd);
+            }
+        }
+        if (a.cg) {
+            const float gv = a.coef * d;
+            a.cg[row * a.W + c] = a.accumulate ? a.cg[row * a.W + c] + gv : gv;
+        }
+    }
+    sd = wave_sum(sd);
+    if ((tid & 63) == 0) red[tid >> 6] = sd;
+    __syncthreads();
+    if (tid == 0 && a.lpart)
+        a.lpart[(size_t)b * a.lstride + (blockIdx.x - b * tilesPer)] = red[0] + red[1] + red[2] + red[3];
+}
+
+// parts[b] = (content + lambd*style, content, style, 0)
+__global__ void __launch_bounds__(256) k_finalize(float* parts, const float* cpart, int ncpart,
+                                                  float cscale, const float* spart, int nspart,
+                                                  float sscale, float lambd) {
+    __shared__ float red[2][4];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    float cs = 0.f, st = 0.f;
+    if (cpart)
+        for (int i = tid; i < ncpart; i += 256) cs += cpart[(size_t)b * ncpart + i];
+    if (spart)
+        for (int i = tid; i < nspart; i += 256) st += spart[(size_t)b * nspart + i];
+    cs = wave_sum(cs);
+    st = wave_sum(st);
+    if ((tid & 63) == 0) { red[0][tid >> 6] = cs; red[1][tid >> 6] = st; }
+    __syncthreads();
+    if (tid == 0) {
+        const float content = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) * cscale;
+        const float style = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) * sscale;
+        parts[b * 4 + 0] = content + lambd * style;
+        parts[b * 4 + 1] = content;
+        parts[b * 4 + 2] = style;
+        parts[b * 4 + 3] = 0.f;
+    }
+}
+
+void launch_gram_fwd(const GramArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_gram_fwd, dim3(a.B * a.nchunk * (C / GCH)), dim3(256), 0, s, a);
+}
+void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_gram_bwd, dim3(a.B * a.nchunk * (C / GCH)), dim3(256), 0, s, a);
+}
+void launch_style_ours(const StyleArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_style_ours, dim3(a.B * (C / 4)), dim3(256), 0, s, a);
+}
+void launch_content(const ContentArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_content, dim3(a.B * (a.T / CROWS)), dim3(256), 0, s, a);
+}
+void launch_finalize(float* parts, const float* cpart, int ncpart, float cscale,
+                     const float* spart, int nspart, float sscale, float lambd, int B,
+                     hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize, dim3(B), dim3(256), 0, s, parts, cpart, ncpart, cscale,
+                       spart, nspart, sscale, lambd);
+}
+
+// Adam on the audio buffer (the north_star's optimiser; bias-corrected, PyTorch semantics).
+__global__ void __launch_bounds__(256) k_adam(float* __restrict__ x, float* __restrict__ m,
+                                              float* __restrict__ v,
+                                              const float* __restrict__ g, size_t n, float lr,
+                                              float b1, float b2, float eps, float bc1,
+                                              float bc2) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float gi = g[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    x[i] -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+}
+
+void launch_adam(float* x, float* m, float* v, const float* g, size_t n, float lr, float b1,
+                 float b2, float eps, float bc1, float bc2, hipStream_t s) {
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, m, v, g,
+                       n, lr, b1, b2, eps, bc1, bc2);
+}
+
+}  // namespace ast

@@ -1,0 +1,179 @@
+"""Batched style-transfer engine: a torch-facing wrapper of one libastyle context.
+
+One ``StyleEngine`` = one HIP context on one GPU holding B independent clips of T samples.
+It replaces, for the hot path, the TF graph + Session that ``GatysNet`` builds
+(methods.py:44-77, 113-137): ``embeds`` is ``get_embeds`` (methods.py:86-95), ``loss_grad``
+is one ScipyOptimizerInterface evaluation (methods.py:167) for every clip at once.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .weights import synthetic_weights
+
+PRECISIONS = {'fp32': 0, 'bf16': 1}
+
+
+def resolve_style_ids(stack=None, style_lyr_ids=None):
+    """methods.py:60-66."""
+    if style_lyr_ids is not None:
+        assert isinstance(style_lyr_ids, (tuple, list)), "style_lyr_ids must be of type tuple or list!"
+        return list(style_lyr_ids)
+    if stack is not None:
+        return list(range(stack * 10, stack * 10 + 10))
+    return list(range(30))
+
+
+class StyleEngine:
+    def __init__(self, batch: int, T: int, cont_ids: Sequence[int], style_ids: Sequence[int],
+                 cnt_channels: int = 128, nb_channels: int = 128, gatys: bool = False,
+                 lambd: float = 100.0, precision: str = 'fp32',
+                 device: Optional[torch.device] = None, weights=None, weight_seed: int = 0):
+        self.lib = _lib.load()
+        if device is None:
+            device = torch.device('cuda', torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != 'cuda':
+            raise _lib.AstError('StyleEngine needs a GPU device (got %s); there is no CPU path'
+                                % self.device)
+        self.batch, self.T = int(batch), int(T)
+        self.cont_ids, self.style_ids = list(cont_ids), list(style_ids)
+        self.gatys = bool(gatys)
+        self.nb_channels = int(nb_channels)
+        self.cnt_channels = int(cnt_channels)
+        self.lambd = float(lambd)
+        cfg = _lib.AstCfg()
+        cfg.batch, cfg.T = self.batch, self.T
+        cfg.n_cont = len(self.cont_ids)
+        for k, v in enumerate(self.cont_ids):
+            cfg.cont_ids[k] = v
+        cfg.cnt_channels = self.cnt_channels
+        cfg.n_style = len(self.style_ids)
+        for k, v in enumerate(self.style_ids):
+            cfg.style_ids[k] = v
+        cfg.nb_channels = self.nb_channels
+        cfg.gatys = int(self.gatys)
+        cfg.precision = PRECISIONS[precision]
+        cfg.lambd = self.lambd
+        self.precision = precision
+        self._cfg = cfg
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            torch.cuda.init()
+            _lib.check(self.lib.ast_create(ctypes.byref(cfg), self.device.index or 0,
+                                           ctypes.byref(h)))
+        self.h = h
+        self.ncc = self.lib.ast_content_cols(self.h)
+        self._targets = None
+        self.set_weights(weights if weights is not None else synthetic_weights(weight_seed))
+
+    # ------------------------------------------------------------------ plumbing
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _ptr(self, t: Optional[torch.Tensor]):
+        if t is None:
+            return None
+        assert t.is_cuda and t.device == self.device and t.dtype == torch.float32, t
+        assert t.is_contiguous()
+        return ctypes.c_void_p(t.data_ptr())
+
+    def _x(self, x: torch.Tensor) -> torch.Tensor:
+        if x.shape != (self.batch, self.T):
+            raise ValueError('x must be [%d, %d], got %s' % (self.batch, self.T, tuple(x.shape)))
+        return x.contiguous()
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.lib.ast_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ API
+    def set_weights(self, weights) -> None:
+        """Upload encoder variables by TF name (Saver.restore, methods.py:79-84).
+        Non-encoder names (the unused decoder) are skipped, as TF never runs them."""
+        for name, arr in weights.items():
+            a = np.ascontiguousarray(np.asarray(arr, dtype=np.float32))
+            rc = self.lib.ast_set_weight(self.h, name.encode(),
+                                         a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), a.size)
+            if rc == -4 and not name.startswith('ae_'):
+                continue
+            _lib.check(rc)
+
+    @property
+    def style_shape(self):
+        L = len(self.style_ids)
+        if self.gatys:
+            return (L, 128, 128)
+        return (min(self.nb_channels, 128), L, L)
+
+    def forward(self, x: torch.Tensor) -> None:
+        _lib.check(self.lib.ast_forward(self.h, self._ptr(self._x(x)), self._stream()))
+
+    def extract(self, i: int) -> torch.Tensor:
+        C = 16 if i == 31 else 128
+        out = torch.empty(self.batch, self.T, C, device=self.device)
+        _lib.check(self.lib.ast_get_extract(self.h, i, self._ptr(out), self._stream()))
+        return out
+
+    def embeds(self, x: torch.Tensor, content: bool = True, style: bool = True):
+        emb_c = torch.empty(self.batch, self.T, self.ncc, device=self.device) if content else None
+        emb_s = torch.empty(self.batch, *self.style_shape, device=self.device) if style else None
+        _lib.check(self.lib.ast_embeds(self.h, self._ptr(self._x(x)), self._ptr(emb_c),
+                                       self._ptr(emb_s), self._stream()))
+        return emb_c, emb_s
+
+    def set_targets(self, phi_c: torch.Tensor, phi_s: torch.Tensor) -> None:
+        """phi_c: [T, ncc] (shared) or [B, T, ncc]; phi_s: style_shape or [B, *style_shape]."""
+        phi_c = phi_c.to(self.device, torch.float32).contiguous()
+        phi_s = phi_s.to(self.device, torch.float32).contiguous()
+        c_shared = phi_c.dim() == 2
+        s_shared = phi_s.dim() == 3
+        if tuple(phi_c.shape[-2:]) != (self.T, self.ncc):
+            raise ValueError('phi_c shape %s != [.., %d, %d]' % (tuple(phi_c.shape), self.T, self.ncc))
+        if tuple(phi_s.shape[-3:]) != tuple(self.style_shape):
+            raise ValueError('phi_s shape %s != [.., %s]' % (tuple(phi_s.shape), self.style_shape))
+        if not c_shared and phi_c.shape[0] != self.batch or not s_shared and phi_s.shape[0] != self.batch:
+            raise ValueError('per-clip targets need a leading batch dimension of %d' % self.batch)
+        self._targets = (phi_c, phi_s)       # keep alive: the context holds raw pointers
+        _lib.check(self.lib.ast_set_targets(self.h, self._ptr(phi_c), int(c_shared),
+                                            self._ptr(phi_s), int(s_shared)))
+
+    def loss_grad(self, x: torch.Tensor, grad: Optional[torch.Tensor] = None,
+                  parts: Optional[torch.Tensor] = None):
+        """Returns (parts [B, 4] = (total, content, style, reg=0), grad [B, T])."""
+        if self._targets is None:
+            raise _lib.AstError('set_targets() first')
+        if grad is None:
+            grad = torch.empty(self.batch, self.T, device=self.device)
+        if parts is None:
+            parts = torch.empty(self.batch, 4, device=self.device)
+        _lib.check(self.lib.ast_loss_grad(self.h, self._ptr(self._x(x)), self._ptr(grad),
+                                          self._ptr(parts), self._stream()))
+        return parts, grad
+
+    def adam_step(self, x, m, v, grad, step, lr=1.0, beta1=0.9, beta2=0.999, eps=1e-8):
+        _lib.check(self.lib.ast_adam_step(self.h, self._ptr(x), self._ptr(m), self._ptr(v),
+                                          self._ptr(grad), int(step), float(lr), float(beta1),
+                                          float(beta2), float(eps), self._stream()))
+
+    def timing(self, enable: bool) -> None:
+        _lib.check(self.lib.ast_timing(self.h, int(enable)))
+
+    def timing_read(self):
+        out = (ctypes.c_float * 7)()
+        _lib.check(self.lib.ast_timing_read(self.h, out, 7))
+        keys = ('block_fwd_ms', 'block_bwd_ms', 'gram_fwd_ms', 'gram_bwd_ms', 'other_ms',
+                'calls', 'blocks')
+        return dict(zip(keys, list(out)))

@@ -1,0 +1,106 @@
+/*
+ * astyle.h — C ABI of libastyle.so, the MI355X (gfx950) implementation of the
+ * winlp4ever/audio_style_transfer optimisation loop's hot path.
+ *
+ * The reference has no FFI: its boundary is Python calling TensorFlow 1.x.  Each entry point
+ * below replaces one reference interface (file:line into the reference):
+ *
+ *   ast_create / ast_destroy  <- GatysNet.build graph construction + tf.Session
+ *                                (methods.py:44-77, 184-188)
+ *   ast_set_weight            <- tf.train.Saver(...).restore(sess, ckpt)  (methods.py:79-84),
+ *                                one variable per call, by TF name (masked.py:141-145)
+ *   ast_forward /             <- cfg.build(...) + cfg.extracts (model.py:57-127) evaluated by
+ *   ast_get_extract              sess.run on extracts[i]
+ *   ast_embeds                <- GatysNet.get_embeds: sess.run(embeds_c | embeds_s)
+ *                                (methods.py:86-95; taps and Gram methods.py:58-76)
+ *   ast_set_targets           <- the phi_c / phi_s constants fed into define_loss
+ *                                (methods.py:113-119, 207-213)
+ *   ast_loss_grad             <- one ScipyOptimizerInterface evaluation: sess.run([loss, grad])
+ *                                of define_loss + tf.gradients w.r.t. x (methods.py:113-137,167)
+ *   ast_adam_step             <- (new) fused optimiser update on the audio buffer; the
+ *                                reference's optimiser is host L-BFGS-B (methods.py:133-137)
+ *
+ * Conventions: every function returns 0 on success and a negative AST_E* code on failure;
+ * ast_last_error() returns a thread-local message.  All buffers named *_dev are device
+ * pointers owned by the caller; the context owns weights and the activation workspace
+ * (sized at create).  No entry point allocates after ast_create, so ast_loss_grad and
+ * ast_adam_step are hipGraph-capturable.  A context is bound to one device and is not
+ * re-entrant; the stream is passed per call (NULL = legacy default stream).
+ */
+#ifndef ASTYLE_H
+#define ASTYLE_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AST_OK 0
+#define AST_E_ARG (-1)      /* invalid argument / configuration */
+#define AST_E_HIP (-2)      /* HIP runtime error */
+#define AST_E_STATE (-3)    /* call order violated (e.g. loss before targets) */
+#define AST_E_NAME (-4)     /* unknown weight name or wrong element count */
+
+#define AST_MAX_TAPS 32
+
+typedef struct ast_ctx ast_ctx;
+
+typedef struct ast_cfg {
+    int batch;                       /* clips per context (the reference: 1) */
+    int T;                           /* samples per clip (--batch_size), multiple of 512 */
+    int n_cont;                      /* --cont_lyrs count            (methods.py:254) */
+    int cont_ids[AST_MAX_TAPS];      /* extract ids 0..31            (methods.py:58) */
+    int cnt_channels;                /* --cnt_channels               (methods.py:259) */
+    int n_style;                     /* resolved style layer count   (methods.py:60-66) */
+    int style_ids[AST_MAX_TAPS];     /* extract ids 0..30 */
+    int nb_channels;                 /* --channels                   (methods.py:75,258) */
+    int gatys;                       /* --gatys                      (methods.py:68-71) */
+    int precision;                   /* 0 = fp32 storage + fp32 MFMA; 1 = bf16 storage + bf16 MFMA */
+    float lambd;                     /* --lambd                      (methods.py:125) */
+} ast_cfg;
+
+/* Context lifetime. */
+int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out);
+void ast_destroy(ast_ctx* ctx);
+int ast_workspace_bytes(const ast_cfg* cfg, size_t* out_bytes);
+
+/* Weights, HWIO float32 host arrays named as the TF variables ("ae_dilatedconv_7/W",
+ * "ae_res_7/biases", "ae_startconv/W", "ae_bottleneck/W", ...). n = element count. */
+int ast_set_weight(ast_ctx* ctx, const char* tf_name, const float* host, size_t n);
+
+/* Encoder forward over x_dev [batch, T] (mu-law units, methods.py:49-54). */
+int ast_forward(ast_ctx* ctx, const float* x_dev, void* stream);
+/* Copy extracts[id] (after ast_forward) to out_dev as float32 [batch, T, C] (C = 16 for id 31). */
+int ast_get_extract(ast_ctx* ctx, int extract_id, float* out_dev, void* stream);
+
+/* Forward + taps: emb_c_dev [batch, T, n_cont_cols]; emb_s_dev [batch, nb, L, L] (ours) or
+ * [batch, L, 128, 128] (Gatys), l2-normalised.  Either output may be NULL. */
+int ast_embeds(ast_ctx* ctx, const float* x_dev, float* emb_c_dev, float* emb_s_dev, void* stream);
+int ast_content_cols(ast_ctx* ctx);  /* n_cont_cols of emb_c */
+
+/* Targets (device pointers, caller keeps them alive).  *_shared != 0: one target for all clips. */
+int ast_set_targets(ast_ctx* ctx, const float* phi_c_dev, int phi_c_shared,
+                    const float* phi_s_dev, int phi_s_shared);
+
+/* One loss+grad evaluation of every clip: grad_dev [batch, T] (d loss / d x, gamma term
+ * excluded), parts_dev [batch, 4] = (content + lambd*style, content, style, 0). */
+int ast_loss_grad(ast_ctx* ctx, const float* x_dev, float* grad_dev, float* parts_dev, void* stream);
+
+/* Fused Adam on the audio buffer: m, v, x updated in place from grad_dev. step >= 1. */
+int ast_adam_step(ast_ctx* ctx, float* x_dev, float* m_dev, float* v_dev, const float* grad_dev,
+                  int step, float lr, float beta1, float beta2, float eps, void* stream);
+
+/* Per-kernel-family device timing (HIP events on the call's stream).  enable!=0 starts
+ * recording; ast_timing_read fills out[0..n) with milliseconds summed since enable for
+ * {block fwd, block bwd, gram fwd, gram bwd, other} and out[5] = number of ast_loss_grad
+ * calls timed, out[6] = launches per family per call (blocks). */
+int ast_timing(ast_ctx* ctx, int enable);
+int ast_timing_read(ast_ctx* ctx, float* out, int n);
+
+const char* ast_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ASTYLE_H */

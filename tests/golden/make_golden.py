@@ -1,0 +1,128 @@
+"""Generate the committed golden fixtures (run in the BUILD container only).
+
+Part 1 — reference-pinned vectors.  ``/root/reference/utils.py`` cannot be imported here
+(it imports tensorflow, librosa and sklearn.decomposition.nmf at module level; ordinary
+ImportErrors, no permission denial — SURVEY §8c).  Its mu-law codecs and output-path naming
+are pure numpy/os, so this script parses the file with ``ast``, takes exactly those
+function definitions (and the two module-level tables they read), and executes them
+unmodified in a namespace holding only numpy/os/time.  No stand-in library is written.
+The reference's text is NOT committed; only the input/output vectors are
+(``reference_vectors.npz`` / ``reference_paths.json``).
+
+Part 2 — oracle vectors at small T (``oracle_T2048.npz``): inputs, loss parts and the
+fp64 gradient of ``oracle/astyle_oracle.py``, for the GPU parity tests.  The oracle itself is
+"parity unpinned" against TF (see its header).
+
+Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import argparse
+import ast
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference'
+
+
+def _load_reference_functions():
+    src = open(os.path.join(REF, 'utils.py')).read()
+    tree = ast.parse(src)
+    keep_fn = {'mu_law_numpy', 'inv_mu_law_numpy', 'gt_s_path', 'crt_t_fol'}
+    keep_assign = {'ins', 'abbrevs'}
+    body = []
+    for node in tree.body:
+        if isinstance(node, ast.FunctionDef) and node.name in keep_fn:
+            body.append(node)
+        elif isinstance(node, ast.Assign) and any(
+                isinstance(t, ast.Name) and t.id in keep_assign for t in node.targets):
+            body.append(node)
+    mod = ast.Module(body=body, type_ignores=[])
+    ns = {'np': np, 'os': os, 'time': time}
+    exec(compile(mod, os.path.join(REF, 'utils.py'), 'exec'), ns)
+    return ns
+
+
+def reference_vectors():
+    ref = _load_reference_functions()
+    rng = np.random.default_rng(1234)
+    # mu_law inputs: edge values, values around every quantisation boundary, random audio
+    edges = np.array([0.0, -0.0, 1.0, -1.0, 1e-9, -1e-9, 0.5, -0.5, 0.999999, -0.999999])
+    q = np.arange(-128, 129, dtype=np.float64)
+    # exact boundaries: x with 128*ln(1+255|x|)/ln256 == k
+    bnd = np.sign(q) * (np.power(256.0, np.abs(q) / 128.0) - 1) / 255.0
+    near = np.concatenate([bnd, np.nextafter(bnd, 2), np.nextafter(bnd, -2)])
+    audio = rng.uniform(-1, 1, 4096)
+    mu_in = np.concatenate([edges, near, audio]).astype(np.float64)
+    mu_in32 = mu_in.astype(np.float32)
+    mu_out = ref['mu_law_numpy'](mu_in)
+    mu_out32 = ref['mu_law_numpy'](mu_in32)
+    # inverse: integer codes, continuous values the optimiser produces, zero
+    inv_in = np.concatenate([q, rng.normal(0, 40, 4096), [0.0, -0.5, 0.5, 200.0, -300.0]])
+    inv_out = ref['inv_mu_law_numpy'](inv_in)
+    np.savez_compressed(os.path.join(HERE, 'reference_vectors.npz'),
+                        mu_in=mu_in, mu_out=mu_out, mu_in32=mu_in32, mu_out32=mu_out32,
+                        inv_in=inv_in, inv_out=inv_out)
+
+    # output-dir naming (utils.py:18-64) for the methods.py argparse namespaces
+    cases = [
+        dict(cont_fn='pachelbel', style_fn='organ', epochs=100, batch_size=16384, sr=16000,
+             stack=0, cont_lyrs=[25], style_lyrs=None, lambd=100.0, gamma=0.0, channels=128,
+             cnt_channels=128, start=1.0, gatys=False, ckpt_path='x', dir='d', outdir='o',
+             logdir='l', cmt=None),
+        dict(cont_fn='a', style_fn='b', epochs=3, batch_size=8192, sr=22050, stack=None,
+             cont_lyrs=[25, 31], style_lyrs=[3, 7], lambd=0.5, gamma=0.1, channels=64,
+             cnt_channels=16, start=2.5, gatys=True, ckpt_path='x', dir='d', outdir='o',
+             logdir='l', cmt='hello'),
+    ]
+    out = []
+    with tempfile.TemporaryDirectory() as td:
+        for kw in cases:
+            p = ref['gt_s_path'](td, **dict(kw))
+            out.append({'kwargs': kw, 'path': os.path.relpath(p, td)})
+    with open(os.path.join(HERE, 'reference_paths.json'), 'w') as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
+def oracle_vectors():
+    sys.path.insert(0, REPO)
+    from oracle import astyle_oracle as O
+    from audio_style_transfer_amd.weights import synthetic_weights, synthetic_clips
+    W = synthetic_weights(0)
+    T = 2048
+    out = {}
+    for tag, kw in [('ours', dict(cont_ids=[25], style_ids=list(range(30)), gatys=False,
+                                  nb_channels=128, cnt_channels=128)),
+                    ('c1', dict(cont_ids=[25], style_ids=list(range(10)), gatys=False,
+                                nb_channels=128, cnt_channels=128)),
+                    ('gatys', dict(cont_ids=[29], style_ids=list(range(30)), gatys=True,
+                                   nb_channels=128, cnt_channels=128)),
+                    ('trunc', dict(cont_ids=[25, 31], style_ids=[3, 7], gatys=False,
+                                   nb_channels=64, cnt_channels=16))]:
+        xc = O.mu_law_numpy(synthetic_clips(1, T, 1000)[0])
+        xs = O.mu_law_numpy(synthetic_clips(1, T, 5000)[0])
+        phi_c, phi_s = O.targets_from_audio(W, xc, [xs], [xc], **kw)
+        rng = np.random.default_rng(7)
+        x = (O.mu_law_numpy(synthetic_clips(1, T, 42)[0]) + rng.normal(0, 4, T))
+        parts, g = O.loss_and_grad(x, W, phi_c=phi_c, phi_s=phi_s, lambd=100.0, gamma=0.0, **kw)
+        out[tag + '_x'] = x
+        out[tag + '_parts'] = parts
+        out[tag + '_grad'] = g
+    np.savez_compressed(os.path.join(HERE, 'oracle_T2048.npz'), **out)
+
+
+if __name__ == '__main__':
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--skip-reference', action='store_true')
+    a = ap.parse_args()
+    if not a.skip_reference:
+        reference_vectors()
+    oracle_vectors()
+    print('fixtures written to', HERE)
