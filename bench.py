@@ -1,0 +1,230 @@
+#!/usr/bin/env python
+"""Benchmark: style-transfer iters/sec on a 256x16384-sample batch, 30-layer WaveNet encoder
+(BASELINE.json metric; workload = configs[2]: 256 clips x 16384 samples per GPU, channel-wise
+Gram over all 30 layers, content layer 29, lambda 100, gamma 0).
+
+One step = one loss+grad evaluation of every clip (encoder fwd -> Gram -> losses -> backward
+to the audio, ast_loss_grad) + the fused Adam update of the audio (ast_adam_step), inputs
+already resident in HBM.  N GPUs = N processes (torch.distributed.run), each owning its own
+256 clips: weak scaling, no collective in the step; the barrier/max-over-ranks
+timing is the only cross-rank traffic.
+
+Prints ONE JSON line on rank 0.  value = (clips processed by all ranks / 256) / seconds.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32 MFMA (= vector) peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0    # dense bf16
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--clips', type=int, default=256, help='clips per GPU (batch)')
+    ap.add_argument('--T', type=int, default=16384)
+    ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
+    ap.add_argument('--lr', type=float, default=2.0)
+    ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0,
+                    help='CPU oracle sample budget (0 disables)')
+    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'),
+                    help='per-launch HBM bytes measured by rocprofv3 --pmc (see DESIGN.md)')
+    return ap.parse_args()
+
+
+def dist_setup():
+    ws = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(0)
+    return ws, rank, local
+
+
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(v, ws):
+    if ws == 1:
+        return v
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device='cuda')
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_problem(eng, B, T, rank, dev):
+    """Synthetic per-clip targets: content clip c_b, style clip s_b;
+    phi_c = emb_c(c_b); phi_s = l2norm(G^(c_b) + G^(s_b) - G^(c_b)) (methods.py:207-212 with
+    one clip per file)."""
+    from audio_style_transfer_amd.weights import synthetic_clips
+    from audio_style_transfer_amd.utils import mu_law_numpy
+    cont = torch.tensor(mu_law_numpy(synthetic_clips(B, T, 1000 + rank * B)), dtype=torch.float32,
+                        device=dev)
+    sty = torch.tensor(mu_law_numpy(synthetic_clips(B, T, 5000 + rank * B)), dtype=torch.float32,
+                       device=dev)
+    phi_c, g_c = eng.embeds(cont)
+    _, g_s = eng.embeds(sty, content=False)
+    phi = g_c + g_s - g_c
+    phi = phi / phi.pow(2).sum(dim=(-2, -1), keepdim=True).clamp_min(1e-12).sqrt()
+    eng.set_targets(phi_c, phi)
+    x = (cont + torch.randn_like(cont) * 4.0).contiguous()
+    return x
+
+
+def cpu_baseline(T, budget_s):
+    """Time the CPU oracle (oracle/astyle_oracle.py, numpy fp32, host BLAS threads) on a
+    bounded sample of the same workload: whole loss+grad evaluations of single clips."""
+    from oracle import astyle_oracle as O
+    from audio_style_transfer_amd.weights import synthetic_weights, synthetic_clips
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get('num_threads', 1) for i in threadpool_info()] or [1])
+    except Exception:
+        cores = 1
+    W = synthetic_weights(0)
+    kw = dict(cont_ids=[29], style_ids=list(range(30)), gatys=False, nb_channels=128,
+              cnt_channels=128)
+    xc = O.mu_law_numpy(synthetic_clips(1, T, 1000)[0])
+    ext, _ = O.encoder_forward(xc, W, 30, dtype=np.float32)
+    phi_c = O.content_embeds(ext, [29], 128)
+    phi_s = O.style_embeds(ext, list(range(30)))
+    x = xc + np.random.default_rng(0).normal(0, 4, T)
+    n = 0
+    t0 = time.time()
+    while True:
+        O.loss_and_grad(x, W, phi_c=phi_c, phi_s=phi_s, lambd=100.0, dtype=np.float32, **kw)
+        n += 1
+        el = time.time() - t0
+        if el >= budget_s or n >= 64:
+            break
+    clip_evals_per_s = n / el
+    return {'value': clip_evals_per_s / 256.0, 'unit': 'iters/s (256x%d batch)' % T,
+            'cores': int(cores), 'kind': 'port',
+            'sample': '%d full loss+grad evaluations of one %d-sample clip (numpy fp32 oracle, '
+                      '30 blocks, ours-Gram L=30) in %.1f s = %.3f clip-evals/s; scaled to the '
+                      '256-clip batch' % (n, T, el, clip_evals_per_s),
+            'clip_evals_per_s': clip_evals_per_s}
+
+
+def main():
+    args = parse()
+    ws, rank, local = dist_setup()
+    dev = torch.device('cuda', local)
+    from audio_style_transfer_amd.engine import StyleEngine
+    B, T = args.clips, args.T
+    cont_ids, style_ids = [29], list(range(30))
+    eng = StyleEngine(B, T, cont_ids, style_ids, precision=args.precision, device=dev,
+                      lambd=100.0)
+    x = make_problem(eng, B, T, rank, dev)
+    m = torch.zeros_like(x)
+    v = torch.zeros_like(x)
+    grad = torch.empty_like(x)
+    parts = torch.empty(B, 4, device=dev)
+    step = 0
+
+    def one_step():
+        nonlocal step
+        step += 1
+        eng.loss_grad(x, grad, parts)
+        eng.adam_step(x, m, v, grad, step, lr=args.lr)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    first_loss = parts[:, 0].mean().item()
+    eng.timing(True)
+    barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    barrier(ws)
+    el = time.perf_counter() - t0
+    el = max_over_ranks(el, ws)
+    tm = eng.timing_read()
+    eng.timing(False)
+    last_loss = parts[:, 0].mean().item()
+    if not np.isfinite(last_loss):
+        raise SystemExit('non-finite loss')
+
+    if rank != 0:
+        barrier(ws)
+        return
+    value = ws * B * args.steps / 256.0 / el
+    calls = max(tm['calls'], 1)
+    nblk = tm['blocks']
+    fwd_ms = tm['block_fwd_ms'] / (calls * nblk)
+    bwd_ms = tm['block_bwd_ms'] / (calls * nblk)
+    launch_ms = (fwd_ms + bwd_ms) / 2
+    flops_per_launch = 131072.0 * T * B          # 2*(384+128)*128 flop per row, fwd or bwd
+    achieved_tflops = flops_per_launch / (launch_ms * 1e-3) / 1e12
+    peak = FP32_MFMA_PEAK_TFLOPS if args.precision == 'fp32' else BF16_MFMA_PEAK_TFLOPS
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get('precision') == args.precision and tj.get('clips') == B and tj.get('T') == T:
+            traffic = tj['block_bytes_per_launch']
+    except Exception:
+        traffic = None
+    gram_fwd_ms = tm['gram_fwd_ms'] / calls
+    gram_bwd_ms = tm['gram_bwd_ms'] / calls
+    L = len(style_ids)
+    gram_bytes = L * B * T * 128 * 4.0
+    out = {
+        'metric': 'style-transfer iters/sec, 256x16384-sample batch, 30-layer WaveNet encoder',
+        'value': value, 'unit': 'iters/s', 'n_gpus': ws, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': el / args.steps * 1e3,
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': args.precision,
+        'data': 'synthetic (seeded sinusoid+noise clips, seeded uniform_unit_scaling weights)',
+        'config': {'workload': 'configs[2]: %dx%d clips per GPU, 30-block encoder, ours-Gram '
+                               'L=30, cont_lyrs [29], lambd 100, gamma 0, Adam step' % (B, T),
+                   'global_batch_clips': ws * B, 'T': T, 'parallelism': 'clip-sharded x%d' % ws,
+                   'precision': args.precision},
+        'clip_iters_per_s': value * 256.0,
+        'roofline': {'kernel': 'k_block_fwd/k_block_bwd (fused dilated conv + 1x1 + epilogues)',
+                     'bound': 'mfma', 'achieved': achieved_tflops, 'peak': peak,
+                     'unit': 'TFLOP/s', 'frac': achieved_tflops / peak, 'traffic': traffic,
+                     'flops_per_launch': flops_per_launch, 'avg_launch_ms': launch_ms,
+                     'fwd_launch_ms': fwd_ms, 'bwd_launch_ms': bwd_ms},
+        'kernels_ms_per_step': {'block_fwd': tm['block_fwd_ms'] / calls,
+                                'block_bwd': tm['block_bwd_ms'] / calls,
+                                'gram_fwd': gram_fwd_ms, 'gram_bwd': gram_bwd_ms,
+                                'other': tm['other_ms'] / calls},
+        'gram_roofline': {'bound': 'hbm', 'fwd_achieved_GBs': gram_bytes / (gram_fwd_ms * 1e-3) / 1e9,
+                          'bwd_achieved_GBs': 2 * gram_bytes / (gram_bwd_ms * 1e-3) / 1e9,
+                          'peak': HBM_PEAK_GBS},
+        'loss_first_last': [first_loss, last_loss],
+    }
+    if ws == 1 and args.cpu_baseline_seconds > 0:
+        out['cpu_baseline'] = cpu_baseline(T, args.cpu_baseline_seconds)
+    print(json.dumps(out), flush=True)
+    barrier(ws)
+
+
+if __name__ == '__main__':
+    main()

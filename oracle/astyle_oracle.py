@@ -216,10 +216,10 @@ def gram(extracts, style_ids, gatys=False):
     """methods.py:62-73.  ours: [C, L, L] (G[c] = E_c E_c^T); Gatys: [L, C, C]."""
     stl = np.stack([extracts[i] for i in style_ids], axis=0)         # [L, T, C]
     if not gatys:
-        s = np.transpose(stl, (2, 0, 1))                              # [C, L, T]
+        s = np.ascontiguousarray(np.transpose(stl, (2, 0, 1)))        # [C, L, T]
     else:
-        s = np.transpose(stl, (0, 2, 1))                              # [L, C, T]
-    return s @ np.transpose(s, (0, 2, 1))
+        s = np.ascontiguousarray(np.transpose(stl, (0, 2, 1)))        # [L, C, T]
+    return s @ np.ascontiguousarray(np.transpose(s, (0, 2, 1)))
 
 
 def l2_normalize(G, eps=1e-12):
@@ -315,10 +315,11 @@ def loss_and_grad(x, W, *, cont_ids, style_ids, phi_c, phi_s, lambd=100.0, gamma
     dG = l2_normalize_bwd(G, dGn)
     S = dG + np.transpose(dG, (0, 2, 1))
     stl = np.stack([ext[i] for i in style_ids], axis=0)              # [L, T, C]
-    if not gatys:
-        dstl = np.einsum('cij,jtc->itc', S, stl)
-    else:
-        dstl = np.einsum('lij,ltj->lti', S, stl)
+    if not gatys:   # dstl[i,t,c] = sum_j S[c,i,j] stl[j,t,c]
+        sct = np.ascontiguousarray(np.transpose(stl, (2, 0, 1)))       # [C, L, T]
+        dstl = np.transpose(S @ sct, (1, 2, 0))
+    else:           # dstl[l,t,i] = sum_j S[l,i,j] stl[l,t,j]
+        dstl = stl @ np.transpose(S, (0, 2, 1))
     for n_, i in enumerate(style_ids):
         grads[i] = grads.get(i, 0) + dstl[n_]
     g = encoder_backward(cache, W, grads, dtype=dtype)
