@@ -42,6 +42,15 @@ constexpr size_t WD = 0, WDT = 3 * C * C, BD = 6 * C * C, WR = BD + C, WRT = WR 
 constexpr size_t WB_OFF = BLK_OFF + NBLK_MAX * BLK_SZ;   // [128][16]
 constexpr size_t BB_OFF = WB_OFF + C * 16;
 constexpr size_t W_TOTAL = BB_OFF + 16;
+// bf16 copies (precision 1), u16 elements per block
+constexpr size_t WDB = 0, WDTB = 3 * C * C, WRB = 6 * C * C, WRTB = 7 * C * C, BLKB_SZ = 8 * C * C;
+
+uint16_t host_bf16(float f) {   // round to nearest even
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
 
 struct Occ { int ext, tensor, off, ncol; };
 
@@ -57,14 +66,17 @@ struct ast_ctx {
     std::vector<Occ> occ;
     int ncc = 0;
     int nchunk = 1;
-    float* cg_buf[NBLK_MAX + 1] = {};       // content grad per tensor (or null)
+    void* cg_buf[NBLK_MAX + 1] = {};        // content grad per tensor (or null), storage type
     bool tensor_in_style[NBLK_MAX + 1] = {};
     bool tensor_has_direct_content[NBLK_MAX + 1] = {};
     // device memory
     float* wts = nullptr;
-    float* act = nullptr; size_t tstride = 0;
+    u16* wtsb = nullptr;                    // bf16 weight copies (precision 1)
+    bool bf = false;                        // precision 1: bf16 activations/gradients
+    size_t esz = 4;                         // bytes per stored element
+    void* act = nullptr; size_t tstride = 0;
     uint32_t* mu = nullptr; uint32_t* me = nullptr;
-    float* chain[2] = {};
+    void* chain[2] = {};
     float* bott = nullptr; float* gbott = nullptr;
     float* gpart = nullptr; float* smat = nullptr; float* spart = nullptr; float* cpart = nullptr;
     int ncpart = 0;
@@ -92,7 +104,7 @@ int plan(const ast_cfg* c, ast_ctx* x) {
     if (c->cnt_channels < 1 || c->nb_channels < 1)
         return fail(AST_E_ARG, "cnt_channels / nb_channels must be >= 1");
     if (c->gatys) return fail(AST_E_ARG, "gatys Gram is not built in this version");
-    if (c->precision != 0) return fail(AST_E_ARG, "only precision 0 (fp32) is built in this version");
+    if (c->precision != 0 && c->precision != 1) return fail(AST_E_ARG, "precision must be 0 (fp32) or 1 (bf16)");
     int top = 0;
     x->need_bott = false;
     x->ncc = 0;
@@ -138,15 +150,16 @@ int plan(const ast_cfg* c, ast_ctx* x) {
 
 size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     const size_t BTC = (size_t)c->batch * c->T * C;
+    const size_t es = c->precision == 1 ? 2 : 4;
     size_t n = 0;
-    n += W_TOTAL * 4;
-    n += (size_t)(x->nblk + 1) * BTC * 4;                   // act
+    n += W_TOTAL * 4 + (size_t)NBLK_MAX * BLKB_SZ * 2;
+    n += (size_t)(x->nblk + 1) * BTC * es;                  // act
     n += 2 * (size_t)x->nblk * c->batch * c->T * 16;        // mu, me
-    n += 2 * BTC * 4;                                       // chain
+    n += 2 * BTC * es;                                      // chain
     int ncg = 0;
     for (int t = 0; t <= NBLK_MAX; ++t)
         if (x->tensor_has_direct_content[t] || (t == 30 && x->need_bott)) ++ncg;
-    n += (size_t)ncg * BTC * 4;
+    n += (size_t)ncg * BTC * es;
     if (x->need_bott) n += 2 * (size_t)c->batch * c->T * 16 * 4;
     n += (size_t)c->batch * x->nchunk * C * 1024 * 4;       // gpart
     n += (size_t)c->batch * C * 1024 * 4;                   // smat
@@ -169,29 +182,51 @@ void tmark(ast_ctx* x, hipStream_t s) {
 }
 
 float* blkw(ast_ctx* x, int l) { return x->wts + BLK_OFF + (size_t)l * BLK_SZ; }
+u16* blkwb(ast_ctx* x, int l) { return x->wtsb + (size_t)l * BLKB_SZ; }
+void* tens(ast_ctx* x, int t) { return (char*)x->act + (size_t)t * x->tstride * x->esz; }
 
 int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
     const ast_cfg& c = x->cfg;
-    launch_startconv_fwd(xd, x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s);
+    if (x->bf) launch_startconv_fwd((const float*)xd, (u16*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s);
+    else launch_startconv_fwd((const float*)xd, (float*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s);
     if (mark) tmark(x, s);
     for (int l = 0; l < x->nblk; ++l) {
-        FwdArgs a;
         float* w = blkw(x, l);
-        a.ein = x->act + (size_t)l * x->tstride;
-        a.eout = x->act + (size_t)(l + 1) * x->tstride;
-        a.wd = w + WD; a.bd = w + BD; a.wr = w + WR; a.br = w + BR;
-        a.mu = x->mu + (size_t)l * c.batch * c.T * 4;
-        a.me = x->me + (size_t)l * c.batch * c.T * 4;
-        a.B = c.batch; a.T = c.T; a.d = 1 << (l % 10); a.n = c.T / a.d;
-        launch_block_fwd(a, s);
+        const int d = 1 << (l % 10);
+        uint32_t* mu = x->mu + (size_t)l * c.batch * c.T * 4;
+        uint32_t* me = x->me + (size_t)l * c.batch * c.T * 4;
+        if (x->bf) {
+            FwdArgsB a;
+            u16* wb = blkwb(x, l);
+            a.ein = (const u16*)tens(x, l); a.eout = (u16*)tens(x, l + 1);
+            a.wdT = wb + WDTB; a.bd = w + BD; a.wrT = wb + WRTB; a.br = w + BR;
+            a.mu = mu; a.me = me;
+            a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
+            launch_block_fwd_bf16(a, s);
+        } else {
+            FwdArgs a;
+            a.ein = (const float*)tens(x, l); a.eout = (float*)tens(x, l + 1);
+            a.wd = w + WD; a.bd = w + BD; a.wr = w + WR; a.br = w + BR;
+            a.mu = mu; a.me = me;
+            a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
+            launch_block_fwd(a, s);
+        }
     }
     if (mark) tmark(x, s);
-    if (x->need_bott)
-        launch_bottleneck_fwd(x->act + (size_t)30 * x->tstride, x->bott, x->wts + WB_OFF,
-                              x->wts + BB_OFF, c.batch, c.T, s);
+    if (x->need_bott) {
+        if (x->bf) launch_bottleneck_fwd((const u16*)tens(x, 30), x->bott, x->wts + WB_OFF, x->wts + BB_OFF, c.batch, c.T, s);
+        else launch_bottleneck_fwd((const float*)tens(x, 30), x->bott, x->wts + WB_OFF, x->wts + BB_OFF, c.batch, c.T, s);
+    }
     HIPCHK(hipGetLastError());
     x->fwd_done = true;
     return 0;
+}
+
+void launch_gram_fwd_any(ast_ctx* x, const GramArgs& g, hipStream_t s) {
+    if (x->bf) launch_gram_fwd_bf16(g, s); else launch_gram_fwd(g, s);
+}
+void launch_gram_bwd_any(ast_ctx* x, const GramArgs& g, hipStream_t s) {
+    if (x->bf) launch_gram_bwd_bf16(g, s); else launch_gram_bwd(g, s);
 }
 
 GramArgs gram_args(ast_ctx* x) {
@@ -247,15 +282,19 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     x->tstride = BTC;
     void* p;
 #define ALLOC(dst, bytes) do { if ((rc = dalloc(x, &p, (bytes)))) { ast_destroy(x); return rc; } dst = (decltype(dst))p; } while (0)
+    x->bf = c.precision == 1;
+    x->esz = x->bf ? 2 : 4;
     ALLOC(x->wts, W_TOTAL * 4);
     (void)hipMemset(x->wts, 0, W_TOTAL * 4);
-    ALLOC(x->act, (size_t)(x->nblk + 1) * BTC * 4);
+    ALLOC(x->wtsb, (size_t)NBLK_MAX * BLKB_SZ * 2);
+    (void)hipMemset(x->wtsb, 0, (size_t)NBLK_MAX * BLKB_SZ * 2);
+    ALLOC(x->act, (size_t)(x->nblk + 1) * BTC * x->esz);
     ALLOC(x->mu, (size_t)x->nblk * c.batch * c.T * 16);
     ALLOC(x->me, (size_t)x->nblk * c.batch * c.T * 16);
-    ALLOC(x->chain[0], BTC * 4);
-    ALLOC(x->chain[1], BTC * 4);
+    ALLOC(x->chain[0], BTC * x->esz);
+    ALLOC(x->chain[1], BTC * x->esz);
     for (int t = 0; t <= NBLK_MAX; ++t)
-        if (x->tensor_has_direct_content[t] || (t == 30 && x->need_bott)) ALLOC(x->cg_buf[t], BTC * 4);
+        if (x->tensor_has_direct_content[t] || (t == 30 && x->need_bott)) ALLOC(x->cg_buf[t], BTC * x->esz);
     if (x->need_bott) {
         ALLOC(x->bott, (size_t)c.batch * c.T * 16 * 4);
         ALLOC(x->gbott, (size_t)c.batch * c.T * 16 * 4);
@@ -307,7 +346,11 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                     for (int co = 0; co < C; ++co)
                         tr[(size_t)k * C * C + co * C + ci] = host[(size_t)k * C * C + ci * C + co];
             if ((rc = put(base + WD, host, 3 * C * C))) return rc;
-            return put(base + WDT, tr.data(), 3 * C * C);
+            if ((rc = put(base + WDT, tr.data(), 3 * C * C))) return rc;
+            std::vector<uint16_t> hb(6 * C * C);
+            for (size_t i = 0; i < 3 * C * C; ++i) { hb[i] = host_bf16(host[i]); hb[3 * C * C + i] = host_bf16(tr[i]); }
+            HIPCHK(hipMemcpy(x->wtsb + (size_t)(l - 1) * BLKB_SZ + WDB, hb.data(), 6 * C * C * 2, hipMemcpyHostToDevice));
+            return 0;
         }
         if (!strcmp(tail, "biases")) { if ((rc = need(C))) return rc; return put(base + BD, host, C); }
     }
@@ -319,7 +362,11 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
             for (int ci = 0; ci < C; ++ci)
                 for (int co = 0; co < C; ++co) tr[co * C + ci] = host[ci * C + co];
             if ((rc = put(base + WR, host, C * C))) return rc;
-            return put(base + WRT, tr.data(), C * C);
+            if ((rc = put(base + WRT, tr.data(), C * C))) return rc;
+            std::vector<uint16_t> hb(2 * C * C);
+            for (size_t i = 0; i < C * C; ++i) { hb[i] = host_bf16(host[i]); hb[C * C + i] = host_bf16(tr[i]); }
+            HIPCHK(hipMemcpy(x->wtsb + (size_t)(l - 1) * BLKB_SZ + WRB, hb.data(), 2 * C * C * 2, hipMemcpyHostToDevice));
+            return 0;
         }
         if (!strcmp(tail, "biases")) { if ((rc = need(C))) return rc; return put(base + BR, host, C); }
     }
@@ -343,8 +390,12 @@ int ast_get_extract(ast_ctx* x, int ext, float* out, void* stream) {
     if (ext < 0 || ext > 30) return fail(AST_E_ARG, "extract id out of range");
     const int tns = ext_to_tensor(ext);
     if (tns > x->nblk) return fail(AST_E_ARG, "extract beyond the blocks this context runs");
-    HIPCHK(hipMemcpyAsync(out, x->act + (size_t)tns * x->tstride, x->tstride * 4,
-                          hipMemcpyDeviceToDevice, S(stream)));
+    if (x->bf) {
+        launch_to_f32((const u16*)tens(x, tns), out, x->tstride, S(stream));
+        HIPCHK(hipGetLastError());
+    } else {
+        HIPCHK(hipMemcpyAsync(out, tens(x, tns), x->tstride * 4, hipMemcpyDeviceToDevice, S(stream)));
+    }
     return 0;
 }
 
@@ -360,7 +411,8 @@ int ast_embeds(ast_ctx* x, const float* xd, float* emb_c, float* emb_s, void* st
         for (const Occ& o : x->occ) {
             ContentArgs a;
             memset(&a, 0, sizeof(a));
-            a.e = o.ext == 31 ? x->bott : x->act + (size_t)o.tensor * x->tstride;
+            a.e = o.ext == 31 ? (const void*)x->bott : tens(x, o.tensor);
+            a.e_bf16 = o.ext != 31 && x->bf;
             a.W = o.ext == 31 ? 16 : C;
             a.ncc = x->ncc; a.off = o.off; a.ncol = o.ncol;
             a.embc = emb_c; a.B = c.batch; a.T = c.T;
@@ -369,7 +421,7 @@ int ast_embeds(ast_ctx* x, const float* xd, float* emb_c, float* emb_s, void* st
     }
     if (emb_s) {
         GramArgs g = gram_args(x);
-        launch_gram_fwd(g, s);
+        launch_gram_fwd_any(x, g, s);
         StyleArgs a = style_args(x);
         a.embs = emb_s;
         launch_style_ours(a, s);
@@ -407,7 +459,9 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
         ContentArgs a;
         memset(&a, 0, sizeof(a));
         a.W = o.ext == 31 ? 16 : C;
-        a.e = o.ext == 31 ? x->bott : x->act + (size_t)o.tensor * x->tstride;
+        a.e = o.ext == 31 ? (const void*)x->bott : tens(x, o.tensor);
+        a.e_bf16 = o.ext != 31 && x->bf;
+        a.cg_bf16 = o.ext != 31 && x->bf;
         a.phi = x->phi_c; a.phi_bstride = x->phi_c_shared ? 0 : (size_t)c.T * x->ncc;
         a.ncc = x->ncc; a.off = o.off; a.ncol = o.ncol; a.coef = ccoef;
         if (o.ext == 31) { a.cg = x->gbott; a.accumulate = !first_bott; first_bott = false; }
@@ -416,12 +470,14 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
         a.B = c.batch; a.T = c.T;
         launch_content(a, s);
     }
-    if (x->need_bott)
-        launch_bottleneck_bwd(x->gbott, x->cg_buf[30], x->wts + WB_OFF, !first_cg[30], c.batch, c.T, s);
+    if (x->need_bott) {
+        if (x->bf) launch_bottleneck_bwd(x->gbott, (u16*)x->cg_buf[30], x->wts + WB_OFF, !first_cg[30], c.batch, c.T, s);
+        else launch_bottleneck_bwd(x->gbott, (float*)x->cg_buf[30], x->wts + WB_OFF, !first_cg[30], c.batch, c.T, s);
+    }
     // style (methods.py:62-76, 118-119)
     GramArgs g = gram_args(x);
     tmark(x, s);
-    launch_gram_fwd(g, s);
+    launch_gram_fwd_any(x, g, s);
     tmark(x, s);
     StyleArgs sa = style_args(x);
     sa.phi = x->phi_s;
@@ -429,24 +485,37 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     sa.smat = x->smat; sa.spart = x->spart;
     launch_style_ours(sa, s);
     tmark(x, s);
-    launch_gram_bwd(g, s);
+    launch_gram_bwd_any(x, g, s);
     tmark(x, s);
     // backward chain through the blocks
     for (int l = x->nblk - 1; l >= 0; --l) {
-        BwdArgs a;
         float* w = blkw(x, l);
         const int tin = l + 1;
-        a.gin = (l == x->nblk - 1) ? nullptr : x->chain[(l + 1) & 1];
-        a.din = x->tensor_in_style[tin] ? x->act + (size_t)tin * x->tstride : x->cg_buf[tin];
-        a.gout = x->chain[l & 1];
-        a.wr = w + WR; a.wrT = w + WRT; a.wdT = w + WDT;
-        a.mu = x->mu + (size_t)l * c.batch * c.T * 4;
-        a.me = x->me + (size_t)l * c.batch * c.T * 4;
-        a.B = c.batch; a.T = c.T; a.d = 1 << (l % 10); a.n = c.T / a.d;
-        launch_block_bwd(a, s);
+        const void* gin = (l == x->nblk - 1) ? nullptr : x->chain[(l + 1) & 1];
+        const void* din = x->tensor_in_style[tin] ? tens(x, tin) : x->cg_buf[tin];
+        const uint32_t* mu = x->mu + (size_t)l * c.batch * c.T * 4;
+        const uint32_t* me = x->me + (size_t)l * c.batch * c.T * 4;
+        const int d = 1 << (l % 10);
+        if (x->bf) {
+            BwdArgsB a;
+            u16* wb = blkwb(x, l);
+            a.gin = (const u16*)gin; a.din = (const u16*)din; a.gout = (u16*)x->chain[l & 1];
+            a.wr = wb + WRB; a.wr32 = w + WR; a.wd = wb + WDB;
+            a.mu = mu; a.me = me;
+            a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
+            launch_block_bwd_bf16(a, s);
+        } else {
+            BwdArgs a;
+            a.gin = (const float*)gin; a.din = (const float*)din; a.gout = (float*)x->chain[l & 1];
+            a.wr = w + WR; a.wrT = w + WRT; a.wdT = w + WDT;
+            a.mu = mu; a.me = me;
+            a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
+            launch_block_bwd(a, s);
+        }
     }
     tmark(x, s);
-    launch_startconv_bwd(x->chain[0], grad, x->wts + W0_OFF, c.batch, c.T, s);
+    if (x->bf) launch_startconv_bwd((const u16*)x->chain[0], grad, x->wts + W0_OFF, c.batch, c.T, s);
+    else launch_startconv_bwd((const float*)x->chain[0], grad, x->wts + W0_OFF, c.batch, c.T, s);
     const int nb = std::min(c.nb_channels, C);
     launch_finalize(parts, x->cpart, x->ncpart, 10.0f / ((float)c.T * (float)x->ncc), x->spart, C,
                     1e3f / (float)(nb * x->L * x->L), c.lambd, c.batch, s);

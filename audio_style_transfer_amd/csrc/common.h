@@ -26,6 +26,39 @@ constexpr int GRS = 17;       // Gram LDS row stride (floats)
 constexpr int GLS = GT * GRS + 1;   // Gram LDS layer stride (545: odd -> conflict-free)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned short u16;                 // raw bf16 storage
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+// bf16 path (precision 1) tile geometry
+constexpr int TMB = 128;      // rows per encoder tile
+constexpr int XSB = 136;      // LDS row stride in bf16 (272 B: ds_read_b128 conflict-free)
+constexpr int GTB = 32;       // Gram: time rows per stage
+constexpr int GCB = 32;       // Gram: channels per workgroup
+
+__device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ __forceinline__ float bflo(uint32_t v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ float bfhi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
+__device__ __forceinline__ uint32_t pack2(float a, float b) {   // RNE, v_cvt_pk_bf16_f32
+    bf16x2 v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ u16 f2bf(float a) { return (u16)(pack2(a, 0.f) & 0xffffu); }
+__device__ __forceinline__ uint32_t relu2(uint32_t u) {         // bf16 relu == int16 max(v, 0)
+    s16x2 v = __builtin_bit_cast(s16x2, u);
+    v = __builtin_elementwise_max(v, (s16x2){0, 0});
+    return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ f32x16 mfma_bf16(uint4 a, uint4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                    __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+// generic element access for kernels templated on the storage type (float | u16 = bf16)
+__device__ __forceinline__ float ldv(const float* p, size_t i) { return p[i]; }
+__device__ __forceinline__ float ldv(const u16* p, size_t i) { return bf2f(p[i]); }
+__device__ __forceinline__ void stv(float* p, size_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void stv(u16* p, size_t i, float v) { p[i] = f2bf(v); }
 
 struct FwdArgs {
     const float* ein; float* eout;
@@ -44,11 +77,28 @@ struct BwdArgs {
     int B, T, d, n;
 };
 
+struct FwdArgsB {
+    const u16* ein; u16* eout;
+    const u16* wdT; const float* bd;       // wdT [3][co][ci] bf16
+    const u16* wrT; const float* br;       // wrT [co][ci] bf16
+    uint32_t* mu; uint32_t* me;
+    int B, T, d, n;
+};
+
+struct BwdArgsB {
+    const u16* gin; const u16* din; u16* gout;
+    const u16* wr;     // [ci][co] bf16  (A operand of step 1)
+    const float* wr32; // [ci][co] fp32  (halo rows)
+    const u16* wd;     // [3][ci][co] bf16 (A operand of step 2)
+    const uint32_t* mu; const uint32_t* me;
+    int B, T, d, n;
+};
+
 struct GramArgs {
-    const float* act; size_t tstride;      // tensor u lives at act + uid[u] * tstride
-    float* actw;                            // same base, writable (bwd, in place)
+    const void* act; size_t tstride;       // tensor u lives at act + uid[u] * tstride elements
+    void* actw;                             // same base, writable (bwd, in place)
     int nu; int uid[32];
-    const float* cg[32];                    // content grad per unique tensor (bwd) or null
+    const void* cg[32];                     // content grad per unique tensor (bwd) or null
     float* gpart;                           // [B][nchunk][C][32][32]
     const float* smat;                      // [B][C][32][32]
     int B, T, nchunk;
@@ -65,27 +115,37 @@ struct StyleArgs {
 };
 
 struct ContentArgs {
-    const float* e; int W;                  // tensor [B][T][W]
+    const void* e; int W;                   // tensor [B][T][W] (float, or bf16 when e_bf16)
+    int e_bf16, cg_bf16;
     const float* phi; size_t phi_bstride;   // [B|1][T][ncc]
     int ncc, off, ncol;
     float coef;                             // 10 * 2 / (T * ncc)
-    float* cg; int accumulate;              // [B][T][W]
+    void* cg; int accumulate;               // [B][T][W] (float, or bf16 when cg_bf16)
     float* lpart; size_t lstride;           // partial sums at lpart[b * lstride + tile]
     float* embc;                            // optional: write e[..., :ncol] into emb [B][T][ncc]
     int B, T;
 };
 
 // launchers (encoder.hip / gram.hip / optim.hip)
-void launch_startconv_fwd(const float* x, float* e0, const float* w0, const float* b0,
+template <typename S>
+void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b0,
                           int B, int T, hipStream_t s);
-void launch_startconv_bwd(const float* g0, float* gx, const float* w0, int B, int T,
+template <typename S>
+void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T,
                           hipStream_t s);
 void launch_block_fwd(const FwdArgs& a, hipStream_t s);
 void launch_block_bwd(const BwdArgs& a, hipStream_t s);
-void launch_bottleneck_fwd(const float* e, float* y, const float* wb, const float* bb,
+void launch_block_fwd_bf16(const FwdArgsB& a, hipStream_t s);
+void launch_block_bwd_bf16(const BwdArgsB& a, hipStream_t s);
+template <typename S>
+void launch_bottleneck_fwd(const S* e, float* y, const float* wb, const float* bb,
                            int B, int T, hipStream_t s);
-void launch_bottleneck_bwd(const float* gy, float* ge, const float* wb, int accumulate,
+template <typename S>
+void launch_bottleneck_bwd(const float* gy, S* ge, const float* wb, int accumulate,
                            int B, int T, hipStream_t s);
+void launch_to_f32(const u16* src, float* dst, size_t n, hipStream_t s);
+void launch_gram_fwd_bf16(const GramArgs& a, hipStream_t s);
+void launch_gram_bwd_bf16(const GramArgs& a, hipStream_t s);
 void launch_gram_fwd(const GramArgs& a, hipStream_t s);
 void launch_gram_bwd(const GramArgs& a, hipStream_t s);
 void launch_style_ours(const StyleArgs& a, hipStream_t s);

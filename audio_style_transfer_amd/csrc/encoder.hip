@@ -223,8 +223,10 @@ __global__ void __launch_bounds__(256) k_block_bwd(BwdArgs a) {
 }
 
 // ae_startconv (model.py:88-93): 1 -> 128 channels, K=3, d=1, input x/128 (model.py:82).
+// Thread per (row, 4 channels).
+template <typename S>
 __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__ x,
-                                                       float* __restrict__ e0,
+                                                       S* __restrict__ e0,
                                                        const float* __restrict__ w0,
                                                        const float* __restrict__ b0, int B,
                                                        int T) {
@@ -243,11 +245,16 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
         const int c = q * 4 + j;
         o[j] = (w0[c] * xm + w0[C + c] * x0 + w0[2 * C + c] * xp) + b0[c];
     }
-    *reinterpret_cast<float4*>(e0 + rowi * C + q * 4) = make_float4(o[0], o[1], o[2], o[3]);
+    if constexpr (sizeof(S) == 4) {
+        *reinterpret_cast<float4*>(e0 + rowi * C + q * 4) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+        *reinterpret_cast<uint2*>(e0 + rowi * C + q * 4) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+    }
 }
 
 // d loss / d x = (1/128) sum_k sum_c W0[k][c] g0[t-k+1][c]; one wave per sample.
-__global__ void __launch_bounds__(256) k_startconv_bwd(const float* __restrict__ g0,
+template <typename S>
+__global__ void __launch_bounds__(256) k_startconv_bwd(const S* __restrict__ g0,
                                                        float* __restrict__ gx,
                                                        const float* __restrict__ w0, int B,
                                                        int T) {
@@ -255,15 +262,22 @@ __global__ void __launch_bounds__(256) k_startconv_bwd(const float* __restrict__
     const int lane = threadIdx.x & 63;
     if (wid >= (size_t)B * T) return;
     const int t = (int)(wid % T);
-    const float* base = g0 + (wid - t) * C;
+    const S* base = g0 + (wid - t) * C;
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int tt = t - k + 1;
         if (tt < 0 || tt >= T) continue;
-        const float2 gv = *reinterpret_cast<const float2*>(base + (size_t)tt * C + 2 * lane);
-        s = fmaf(w0[k * C + 2 * lane], gv.x, s);
-        s = fmaf(w0[k * C + 2 * lane + 1], gv.y, s);
+        float g0v, g1v;
+        if constexpr (sizeof(S) == 4) {
+            const float2 gv = *reinterpret_cast<const float2*>(base + (size_t)tt * C + 2 * lane);
+            g0v = gv.x; g1v = gv.y;
+        } else {
+            const uint32_t gv = *reinterpret_cast<const uint32_t*>(base + (size_t)tt * C + 2 * lane);
+            g0v = bflo(gv); g1v = bfhi(gv);
+        }
+        s = fmaf(w0[k * C + 2 * lane], g0v, s);
+        s = fmaf(w0[k * C + 2 * lane + 1], g1v, s);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
@@ -271,7 +285,8 @@ __global__ void __launch_bounds__(256) k_startconv_bwd(const float* __restrict__
 }
 
 // ae_bottleneck (model.py:121-127): 1x1, 128 -> 16.  Thread per (row, out channel).
-__global__ void __launch_bounds__(256) k_bottleneck_fwd(const float* __restrict__ e,
+template <typename S>
+__global__ void __launch_bounds__(256) k_bottleneck_fwd(const S* __restrict__ e,
                                                         float* __restrict__ y,
                                                         const float* __restrict__ wb,
                                                         const float* __restrict__ bb, int B,
@@ -280,15 +295,15 @@ __global__ void __launch_bounds__(256) k_bottleneck_fwd(const float* __restrict_
     if (i >= (size_t)B * T * 16) return;
     const size_t rowi = i >> 4;
     const int j = (int)(i & 15);
-    const float* er = e + rowi * C;
     float s = 0.f;
-    for (int c = 0; c < C; ++c) s = fmaf(er[c], wb[c * 16 + j], s);
+    for (int c = 0; c < C; ++c) s = fmaf(ldv(e, rowi * C + c), wb[c * 16 + j], s);
     y[i] = s + bb[j];
 }
 
 // ge[row][c] (+)= sum_j Wb[c][j] gy[row][j]
+template <typename S>
 __global__ void __launch_bounds__(256) k_bottleneck_bwd(const float* __restrict__ gy,
-                                                        float* __restrict__ ge,
+                                                        S* __restrict__ ge,
                                                         const float* __restrict__ wb,
                                                         int accumulate, int B, int T) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -299,7 +314,13 @@ __global__ void __launch_bounds__(256) k_bottleneck_bwd(const float* __restrict_
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) s = fmaf(wb[c * 16 + j], g[j], s);
-    ge[i] = accumulate ? ge[i] + s : s;
+    stv(ge, i, accumulate ? ldv(ge, i) + s : s);
+}
+
+__global__ void __launch_bounds__(256) k_to_f32(const u16* __restrict__ src, float* __restrict__ dst,
+                                                size_t n) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) dst[i] = bf2f(src[i]);
 }
 
 void launch_block_fwd(const FwdArgs& a, hipStream_t s) {
@@ -308,29 +329,43 @@ void launch_block_fwd(const FwdArgs& a, hipStream_t s) {
 void launch_block_bwd(const BwdArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_block_bwd, dim3(a.B * (a.T / TM)), dim3(256), 0, s, a);
 }
-void launch_startconv_fwd(const float* x, float* e0, const float* w0, const float* b0, int B,
-                          int T, hipStream_t s) {
+template <typename S>
+void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b0, int B, int T,
+                          hipStream_t s) {
     const size_t n = (size_t)B * T * 32;
-    hipLaunchKernelGGL(k_startconv_fwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x,
+    hipLaunchKernelGGL(k_startconv_fwd<S>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x,
                        e0, w0, b0, B, T);
 }
-void launch_startconv_bwd(const float* g0, float* gx, const float* w0, int B, int T,
-                          hipStream_t s) {
+template <typename S>
+void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T, hipStream_t s) {
     const size_t n = (size_t)B * T * 64;
-    hipLaunchKernelGGL(k_startconv_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g0,
+    hipLaunchKernelGGL(k_startconv_bwd<S>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g0,
                        gx, w0, B, T);
 }
-void launch_bottleneck_fwd(const float* e, float* y, const float* wb, const float* bb, int B,
-                           int T, hipStream_t s) {
+template <typename S>
+void launch_bottleneck_fwd(const S* e, float* y, const float* wb, const float* bb, int B, int T,
+                           hipStream_t s) {
     const size_t n = (size_t)B * T * 16;
-    hipLaunchKernelGGL(k_bottleneck_fwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, e,
+    hipLaunchKernelGGL(k_bottleneck_fwd<S>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, e,
                        y, wb, bb, B, T);
 }
-void launch_bottleneck_bwd(const float* gy, float* ge, const float* wb, int accumulate, int B,
-                           int T, hipStream_t s) {
+template <typename S>
+void launch_bottleneck_bwd(const float* gy, S* ge, const float* wb, int accumulate, int B, int T,
+                           hipStream_t s) {
     const size_t n = (size_t)B * T * C;
-    hipLaunchKernelGGL(k_bottleneck_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_bottleneck_bwd<S>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                        gy, ge, wb, accumulate, B, T);
 }
+void launch_to_f32(const u16* src, float* dst, size_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_to_f32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, n);
+}
+template void launch_startconv_fwd<float>(const float*, float*, const float*, const float*, int, int, hipStream_t);
+template void launch_startconv_fwd<u16>(const float*, u16*, const float*, const float*, int, int, hipStream_t);
+template void launch_startconv_bwd<float>(const float*, float*, const float*, int, int, hipStream_t);
+template void launch_startconv_bwd<u16>(const u16*, float*, const float*, int, int, hipStream_t);
+template void launch_bottleneck_fwd<float>(const float*, float*, const float*, const float*, int, int, hipStream_t);
+template void launch_bottleneck_fwd<u16>(const u16*, float*, const float*, const float*, int, int, hipStream_t);
+template void launch_bottleneck_bwd<float>(const float*, float*, const float*, int, int, int, hipStream_t);
+template void launch_bottleneck_bwd<u16>(const float*, u16*, const float*, int, int, int, hipStream_t);
 
 }  // namespace ast

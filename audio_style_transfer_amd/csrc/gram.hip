@@ -23,7 +23,7 @@ __device__ __forceinline__ void gram_stage(float* Et, const GramArgs& a, int b, 
         const int u = i / (GT * 4), rem = i - u * (GT * 4);
         const int tt = rem >> 2, q = rem & 3;
         const float4 v = *reinterpret_cast<const float4*>(
-            a.act + (size_t)a.uid[u] * a.tstride + ((size_t)b * a.T + t0 + tt) * C + c0 + q * 4);
+            (const float*)a.act + (size_t)a.uid[u] * a.tstride + ((size_t)b * a.T + t0 + tt) * C + c0 + q * 4);
         float* dst = &Et[u * GLS + tt * GRS + q * 4];
         dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
     }
@@ -117,13 +117,13 @@ __global__ void __launch_bounds__(256) k_gram_bwd(GramArgs a) {
             const size_t o = (size_t)a.uid[u] * a.tstride + ((size_t)b * a.T + t0 + tt) * C + c0 + q * 4;
             const float* src = &Et[u * GLS + tt * GRS + q * 4];
             float4 v = make_float4(src[0], src[1], src[2], src[3]);
-            const float* cgp = a.cg[u];
+            const float* cgp = (const float*)a.cg[u];
             if (cgp) {
                 const float4 g = *reinterpret_cast<const float4*>(
                     cgp + ((size_t)b * a.T + t0 + tt) * C + c0 + q * 4);
                 v.x += g.x; v.y += g.y; v.z += g.z; v.w += g.w;
             }
-            *reinterpret_cast<float4*>(a.actw + o) = v;
+            *reinterpret_cast<float4*>((float*)a.actw + o) = v;
         }
     }
 }
@@ -217,8 +217,11 @@ __global__ void __launch_bounds__(256) k_style_ours(StyleArgs a) {
 
 // Content taps (methods.py:58,116-117): cg = coef * (E[..., :ncol] - phi[..., off:off+ncol]),
 // partial sums of the squared error per CROWS rows.  Optionally copies the tap into emb.
+template <typename TE, typename TG>
 __global__ void __launch_bounds__(256) k_content(ContentArgs a) {
     __shared__ float red[4];
+    const TE* E = (const TE*)a.e;
+    TG* CG = (TG*)a.cg;
     const int tilesPer = a.T / CROWS;
     const int b = blockIdx.x / tilesPer;
     const int t0 = (blockIdx.x - b * tilesPer) * CROWS;
@@ -227,7 +230,7 @@ __global__ void __launch_bounds__(256) k_content(ContentArgs a) {
     for (int i = tid; i < CROWS * a.W; i += 256) {
         const int tt = i / a.W, c = i - tt * a.W;
         const size_t row = (size_t)b * a.T + t0 + tt;
-        const float e = a.e[row * a.W + c];
+        const float e = ldv(E, row * a.W + c);
         float d = 0.f;
         if (c < a.ncol) {
             if (a.embc) a.embc[row * a.ncc + a.off + c] = e;
@@ -236,9 +239,9 @@ __global__ void __launch_bounds__(256) k_content(ContentArgs a) {
                 sd = fmaf(d, d, sd);
             }
         }
-        if (a.cg) {
+        if (CG) {
             const float gv = a.coef * d;
-            a.cg[row * a.W + c] = a.accumulate ? a.cg[row * a.W + c] + gv : gv;
+            stv(CG, row * a.W + c, a.accumulate ? ldv(CG, row * a.W + c) + gv : gv);
         }
     }
     sd = wave_sum(sd);
@@ -283,7 +286,11 @@ void launch_style_ours(const StyleArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_style_ours, dim3(a.B * (C / 4)), dim3(256), 0, s, a);
 }
 void launch_content(const ContentArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_content, dim3(a.B * (a.T / CROWS)), dim3(256), 0, s, a);
+    const dim3 g(a.B * (a.T / CROWS));
+    if (a.e_bf16 && a.cg_bf16) hipLaunchKernelGGL((k_content<u16, u16>), g, dim3(256), 0, s, a);
+    else if (a.e_bf16) hipLaunchKernelGGL((k_content<u16, float>), g, dim3(256), 0, s, a);
+    else if (a.cg_bf16) hipLaunchKernelGGL((k_content<float, u16>), g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_content<float, float>), g, dim3(256), 0, s, a);
 }
 void launch_finalize(float* parts, const float* cpart, int ncpart, float cscale,
                      const float* spart, int nspart, float sscale, float lambd, int B,

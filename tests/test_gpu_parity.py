@@ -178,3 +178,59 @@ def test_full_size_default_config(weights, dev):
     e = rel(grad[0], ref_g)
     print('full-size grad rel-L2 %.3g' % e)
     assert e <= 2e-3
+
+
+# --------------------------------------------------------------------------- bf16 path
+# Tolerances for precision='bf16' (bf16 storage + bf16 MFMA, fp32 accumulation).  The bf16
+# gradient is the exact gradient of the bf16-rounded network: a CPU emulation
+# (tools/bf16_emulate.py) attributes ~11% rel-L2 of it to forward activation/weight rounding
+# over 30 blocks and ~0.5% to the bf16 backward chain.  Bounds:
+#   extracts / embeddings rel-L2 <= 2e-2, loss parts rel <= 1e-2,
+#   gradient cosine >= 0.98 and rel-L2 <= 0.25.
+@pytest.mark.parametrize('tag', list(CASES))
+def test_bf16_loss_grad_close_to_oracle(tag, weights, golden, dev):
+    T = 2048
+    kw = CASES[tag]
+    phi_c, phi_s = _targets(tag, T, weights)
+    x = golden[tag + '_x']
+    eng = _engine(1, T, kw, weights, precision='bf16')
+    eng.set_targets(torch.tensor(phi_c, dtype=torch.float32), torch.tensor(phi_s, dtype=torch.float32))
+    parts, grad = eng.loss_grad(torch.tensor(x[None], dtype=torch.float32, device=dev))
+    parts = parts.cpu().numpy()[0]
+    grad = grad.cpu().numpy()[0]
+    ref_parts, ref_g = golden[tag + '_parts'], golden[tag + '_grad']
+    for k in range(3):
+        assert abs(parts[k] - ref_parts[k]) <= 1e-2 * abs(ref_parts[k]) + 1e-6, (k, parts, ref_parts)
+    cos = float(np.dot(grad, ref_g) / np.linalg.norm(grad) / np.linalg.norm(ref_g))
+    assert cos >= 0.98 and rel(grad, ref_g) <= 0.25, (cos, rel(grad, ref_g))
+
+
+@pytest.mark.parametrize('T', [512, 2048])
+def test_bf16_extracts_and_embeds(T, weights, dev):
+    kw = dict(CASES['trunc'], cont_ids=[29, 31], style_ids=[0, 9, 30])
+    x = O.mu_law_numpy(synthetic_clips(1, T, 42)[0]) + np.random.default_rng(3).normal(0, 4, T)
+    ext, _ = O.encoder_forward(x, weights, 30, need_bottleneck=True)
+    eng = _engine(1, T, kw, weights, precision='bf16')
+    xt = torch.tensor(x[None], dtype=torch.float32, device=dev)
+    eng.forward(xt)
+    for i in [0, 9, 19, 29, 30, 31]:
+        assert rel(eng.extract(i).cpu().numpy()[0], ext[i]) <= 2e-2, i
+    emb_c, emb_s = eng.embeds(xt)
+    assert rel(emb_c.cpu().numpy()[0], O.content_embeds(ext, kw['cont_ids'], kw['cnt_channels'])) <= 2e-2
+    assert rel(emb_s.cpu().numpy()[0], O.style_embeds(ext, kw['style_ids'], False, kw['nb_channels'])) <= 2e-2
+
+
+def test_bf16_batch_invariance(weights, dev):
+    T = 2048
+    kw = CASES['ours']
+    phi_c, phi_s = _targets('ours', T, weights)
+    xs = O.mu_law_numpy(synthetic_clips(3, T, 77)) + np.random.default_rng(11).normal(0, 4, (3, T))
+    x3 = torch.tensor(xs, dtype=torch.float32, device=dev)
+    eng3 = _engine(3, T, kw, weights, precision='bf16')
+    eng3.set_targets(torch.tensor(phi_c, dtype=torch.float32), torch.tensor(phi_s, dtype=torch.float32))
+    p3, g3 = eng3.loss_grad(x3)
+    eng1 = _engine(1, T, kw, weights, precision='bf16')
+    eng1.set_targets(torch.tensor(phi_c, dtype=torch.float32), torch.tensor(phi_s, dtype=torch.float32))
+    for b in range(3):
+        p1, g1 = eng1.loss_grad(x3[b:b + 1].contiguous())
+        assert torch.equal(p1[0], p3[b]) and torch.equal(g1[0], g3[b]), b

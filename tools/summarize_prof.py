@@ -1,0 +1,71 @@
+"""Summarise a tools/profile.sh run into profiles/ (committed evidence).
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats, verbatim) and
+profiles/<tag>_summary.json: per kernel, average duration and HBM traffic per launch from
+the separate FETCH_SIZE / WRITE_SIZE passes.  gfx950 correction (MI355X_MICROARCH.md §HBM):
+FETCH_SIZE counts half the bytes of a wide (16 B/lane) coalesced read, so fetched bytes =
+2 * FETCH_SIZE * 1024; WRITE_SIZE reads exactly for 16-B stores: written = WRITE_SIZE * 1024.
+Also (re)writes profiles/traffic.json for bench.py's roofline.traffic field.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counters(path, name):
+    per = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row['Counter_Name'] == name:
+                per[row['Kernel_Name']].append(float(row['Counter_Value']))
+    return per
+
+
+def main(tag, precision, clips, T):
+    src = os.path.join(ROOT, 'gpurun_out', 'prof_' + tag)
+    dst = os.path.join(ROOT, 'profiles')
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, 'trace', 'run_kernel_stats.csv'),
+                os.path.join(dst, tag + '_kernel_stats.csv'))
+    stats = {}
+    with open(os.path.join(src, 'trace', 'run_kernel_stats.csv')) as f:
+        for row in csv.DictReader(f):
+            stats[row['Name']] = {'calls': int(row['Calls']), 'avg_ms': float(row['AverageNs']) / 1e6,
+                                  'total_ms': float(row['TotalDurationNs']) / 1e6,
+                                  'pct': float(row['Percentage'])}
+    fetch = counters(os.path.join(src, 'fetch', 'run_counter_collection.csv'), 'FETCH_SIZE')
+    write = counters(os.path.join(src, 'write', 'run_counter_collection.csv'), 'WRITE_SIZE')
+    for k, v in stats.items():
+        if k in fetch:
+            v['fetch_bytes_raw'] = sum(fetch[k]) / len(fetch[k]) * 1024
+            v['fetch_bytes_corrected'] = 2 * v['fetch_bytes_raw']
+        if k in write:
+            v['write_bytes'] = sum(write[k]) / len(write[k]) * 1024
+        if 'fetch_bytes_corrected' in v and 'write_bytes' in v:
+            v['hbm_bytes_per_launch'] = v['fetch_bytes_corrected'] + v['write_bytes']
+            v['hbm_GBs'] = v['hbm_bytes_per_launch'] / (v['avg_ms'] * 1e-3) / 1e9
+    summary = {'tag': tag, 'precision': precision, 'clips': clips, 'T': T, 'kernels': stats}
+    with open(os.path.join(dst, tag + '_summary.json'), 'w') as f:
+        json.dump(summary, f, indent=1)
+    fw, bw = stats.get('k_block_fwd', {}), stats.get('k_block_bwd', {})
+    if 'hbm_bytes_per_launch' in fw and 'hbm_bytes_per_launch' in bw:
+        tj = {'precision': precision, 'clips': clips, 'T': T, 'source': tag,
+              'block_bytes_per_launch': (fw['hbm_bytes_per_launch'] + bw['hbm_bytes_per_launch']) / 2,
+              'fwd_bytes_per_launch': fw['hbm_bytes_per_launch'],
+              'bwd_bytes_per_launch': bw['hbm_bytes_per_launch']}
+        with open(os.path.join(dst, 'traffic.json'), 'w') as f:
+            json.dump(tj, f, indent=1)
+    for k, v in sorted(stats.items(), key=lambda kv: -kv[1]['total_ms'])[:10]:
+        print('%-28s calls %4d avg %8.3f ms  hbm/launch %s' % (
+            k, v['calls'], v['avg_ms'],
+            '%.3f GB (%.0f GB/s)' % (v['hbm_bytes_per_launch'] / 1e9, v['hbm_GBs'])
+            if 'hbm_bytes_per_launch' in v else '-'))
+
+
+if __name__ == '__main__':
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
