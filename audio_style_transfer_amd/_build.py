@@ -25,15 +25,17 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
+    lib = LIB if not stamps else os.path.join(PKG, 'libastyle_stamps.so')
+    if not force and not stamps and not _stale():
         return LIB
-    objdir = os.path.join(PKG, 'build')
+    objdir = os.path.join(PKG, 'build' if not stamps else 'build_stamps')
+    flags = FLAGS + (['-DASTYLE_STAMPS'] if stamps else [])
     os.makedirs(objdir, exist_ok=True)
 
     def cc(src):
         obj = os.path.join(objdir, src.replace('.hip', '.o'))
-        cmd = [HIPCC, *FLAGS, '-c', os.path.join(CSRC, src), '-o', obj]
+        cmd = [HIPCC, *flags, '-c', os.path.join(CSRC, src), '-o', obj]
         if verbose:
             print(' '.join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -45,14 +47,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(len(SOURCES)) as ex:
         objs = list(ex.map(cc, SOURCES))
-    tmp = LIB + '.tmp'
+    tmp = lib + '.tmp'
     cmd = [HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', *objs, '-o', tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError('link failed:\n' + r.stderr)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == '__main__':
-    print(build(force='--force' in sys.argv, verbose=True))
+    print(build(force='--force' in sys.argv, verbose=True, stamps='--stamps' in sys.argv))

@@ -10,7 +10,7 @@ import ctypes
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, 'libastyle.so')
+LIB_PATH = os.environ.get('ASTYLE_LIB', os.path.join(PKG, 'libastyle.so'))
 MAX_TAPS = 32
 
 # Every symbol include/astyle.h declares (checked by tests/test_abi.py).

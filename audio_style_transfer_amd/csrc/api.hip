@@ -17,6 +17,7 @@ using namespace ast;
 namespace {
 
 thread_local std::string g_err;
+unsigned long long* g_stamps = nullptr;   // diagnostic phase stamps (ASTYLE_STAMPS builds)
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -197,6 +198,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
         uint32_t* me = x->me + (size_t)l * c.batch * c.T * 4;
         if (x->bf) {
             FwdArgsB a;
+            a.stamps = g_stamps;
             u16* wb = blkwb(x, l);
             a.ein = (const u16*)tens(x, l); a.eout = (u16*)tens(x, l + 1);
             a.wdT = wb + WDTB; a.bd = w + BD; a.wrT = wb + WRTB; a.br = w + BR;
@@ -257,6 +259,13 @@ StyleArgs style_args(ast_ctx* x) {
 extern "C" {
 
 const char* ast_last_error(void) { return g_err.c_str(); }
+
+// Diagnostic hook (not in astyle.h): device buffer of 12 u64 phase-cycle sums that
+// -DASTYLE_STAMPS builds of the bf16 block kernels accumulate into; NULL disables.
+int ast_debug_stamps(void* dev_u64x12) {
+    g_stamps = (unsigned long long*)dev_u64x12;
+    return 0;
+}
 
 int ast_workspace_bytes(const ast_cfg* cfg, size_t* out) {
     if (!cfg || !out) return fail(AST_E_ARG, "null argument");
@@ -498,6 +507,7 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
         const int d = 1 << (l % 10);
         if (x->bf) {
             BwdArgsB a;
+            a.stamps = g_stamps;
             u16* wb = blkwb(x, l);
             a.gin = (const u16*)gin; a.din = (const u16*)din; a.gout = (u16*)x->chain[l & 1];
             a.wr = wb + WRB; a.wr32 = w + WR; a.wd = wb + WDB;

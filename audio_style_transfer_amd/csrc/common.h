@@ -78,6 +78,7 @@ struct BwdArgs {
 };
 
 struct FwdArgsB {
+    unsigned long long* stamps;            // diagnostic builds (-DASTYLE_STAMPS) only
     const u16* ein; u16* eout;
     const u16* wdT; const float* bd;       // wdT [3][co][ci] bf16
     const u16* wrT; const float* br;       // wrT [co][ci] bf16
@@ -86,6 +87,7 @@ struct FwdArgsB {
 };
 
 struct BwdArgsB {
+    unsigned long long* stamps;            // diagnostic builds (-DASTYLE_STAMPS) only
     const u16* gin; const u16* din; u16* gout;
     const u16* wr;     // [ci][co] bf16  (A operand of step 1)
     const float* wr32; // [ci][co] fp32  (halo rows)

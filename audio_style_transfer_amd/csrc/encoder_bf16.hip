@@ -1,19 +1,30 @@
 // bf16 encoder blocks (precision 1): bf16 storage in HBM, v_mfma_f32_32x32x16_bf16 with fp32
 // accumulation, fp32 epilogue math, RNE rounding on store.  Same algebra as encoder.hip
-// (model.py:95-116 forward, its transpose backward), different mapping:
-//   * both GEMMs run transposed — out^T[channel][row] = W^T[channel][k] * act^T[k][row] — so
-//     the weights are the A operand (one 16-B global/L2 load per lane per k-block, each
-//     weight byte read once per workgroup: wave w owns output channels 32w..32w+31) and the
-//     staged activation rows are the B operand (ds_read_b128 from a 272-B-stride LDS image,
-//     conflict-free);
-//   * a tile is TMB = 128 positions in time_to_batch order (+2 halo rows);
-//   * relu of the input is applied on the B fragment with v_pk_max_i16 (bf16 relu == int16
-//     max with 0), so the raw rows stay in LDS for the residual;
-//   * outputs are written back into the LDS tile and leave as whole 256-B rows.
+// (model.py:95-116 forward, its transpose backward); MI355X-specific mapping:
+//
+//  * Persistent: one 512-thread workgroup per CU walks tiles of TMB = 128 positions (time_to_
+//    batch order, masked.py:57-86).  Wave w owns output channels 32*(w&3).. and tile columns
+//    64*(w>>2)..; its weights (Wd^T: 3 taps x 128 k, Wr^T) sit in 128 VGPRs as MFMA A
+//    fragments for the whole launch, so no weight byte is re-read per tile.
+//  * GEMMs run transposed (out^T = W^T act^T): staged rows are the B operand, read with
+//    ds_read_b128 from a 272-B-stride LDS image (conflict-free).
+//  * Segment layout: each dilation sub-sequence inside a tile gets its own zero pad row on
+//    either side, so the three taps of every column read rows L-1, L, L+1 with no selects
+//    (SAME zero padding, masked.py:139).  Sub-sequences shorter than 32 (small T only) fall
+//    back to per-column tap masks (template MASKED).
+//  * The relu'd copy of the input is staged once (fwd), the next tile's rows are prefetched
+//    into registers while the current tile computes, and outputs leave as whole 256-B rows.
 #include "common.h"
 #include <algorithm>
 
 namespace ast {
+
+constexpr int NRMAX = TMB + 8;                 // LDS rows: TMB + 2 pad rows per segment (M >= 32)
+constexpr int NTH = 512;                       // threads per workgroup (two waves per SIMD)
+constexpr int NW = NTH / 64;                   // waves; 4 channel blocks x (NW/4) column groups
+constexpr int NJ = 16 / NW;                    // 32-column N-tiles per wave
+constexpr int PF_K = (NRMAX * 16 + NTH - 1) / NTH;   // 16-B pieces per thread per tile
+constexpr int PAD = -(1 << 28);                // ROWM entry of a zero (pad) row
 
 __device__ __forceinline__ int pos_to_tb(int p, int n, int d) { return (p % n) * d + p / n; }
 
@@ -21,47 +32,101 @@ __device__ __forceinline__ uint4 relu8(uint4 v) {
     return make_uint4(relu2(v.x), relu2(v.y), relu2(v.z), relu2(v.w));
 }
 
-// accumulator register i of a 32x32 tile holds row (i&3) + 8(i>>2) + 4h (the channel here)
+// accumulator register i of a 32x32 tile holds row (i&3) + 8(i>>2) + 4h (a channel here)
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-// Stage rows p0-1 .. p0+TMB of a clip into an LDS image (16 threads per 256-B row).  With
-// ME != nullptr also emit the e>0 bit masks of the TMB centre rows: each thread turns its 8
-// channels into 8 bits, 4 lanes OR their bytes into a 32-channel word, lane q=0 stores 16 B.
-__device__ __forceinline__ void stage_rows(u16* Xs, const int* TT, const u16* src, size_t cb,
-                                           uint32_t* me, size_t mbase, int tid) {
-    for (int i = tid; i < (TMB + 2) * 16; i += 256) {
-        const int rr = i >> 4, q = i & 15;
-        const int t = TT[rr];
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (t >= 0) v = *reinterpret_cast<const uint4*>(src + cb + (size_t)t * C + q * 8);
-        *reinterpret_cast<uint4*>(&Xs[rr * XSB + q * 8]) = v;
-        if (me) {
-            const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-            uint32_t bits = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                bits |= ((short)(d[k] & 0xffffu) > 0 ? 1u : 0u) << (2 * k);
-                bits |= ((short)(d[k] >> 16) > 0 ? 1u : 0u) << (2 * k + 1);
-            }
-            uint32_t m = bits << (8 * (q & 3));
-            m |= (uint32_t)__shfl_xor((int)m, 1);
-            m |= (uint32_t)__shfl_xor((int)m, 2);
-            const int lane = tid & 63;
-            const uint32_t w1 = (uint32_t)__shfl((int)m, lane + 4);
-            const uint32_t w2 = (uint32_t)__shfl((int)m, lane + 8);
-            const uint32_t w3 = (uint32_t)__shfl((int)m, lane + 12);
-            if (q == 0 && rr >= 1 && rr <= TMB)
-                *reinterpret_cast<uint4*>(me + mbase + (size_t)t * 4) = make_uint4(m, w1, w2, w3);
-        }
-    }
+// Diagnostic phase stamps (guide: In-kernel stamps).  Only -DASTYLE_STAMPS builds execute
+// them; cycle deltas per phase are summed per wave and added to a.stamps[phase] at exit.
+#ifdef ASTYLE_STAMPS
+#define STAMP_DECL unsigned long long st_acc[12] = {}; unsigned long long st_prev = stamp_now();
+#define STAMP(k) { const unsigned long long st_t = stamp_now(); st_acc[k] += st_t - st_prev; st_prev = st_t; }
+#define STAMP_FLUSH(ptr) if (((threadIdx.x & 63) == 0) && (ptr)) { for (int k = 0; k < 12; ++k) atomicAdd(&(ptr)[k], st_acc[k]); }
+__device__ __forceinline__ unsigned long long stamp_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#else
+#define STAMP_DECL
+#define STAMP(k)
+#define STAMP_FLUSH(ptr)
+#endif
+
+struct Layout {            // uniform per launch
+    int M;                 // segment length (positions); TMB when one segment (+ halos)
+    int nrows;             // LDS rows of a tile
+};
+
+__device__ __forceinline__ int rowmap(int c, const Layout& ly) {
+    return (c / ly.M) * (ly.M + 2) + 1 + (c % ly.M);
 }
 
-__device__ __forceinline__ void tile_times(int* TT, int p0, const int T, const int n, const int d,
-                                           int tid) {
-    if (tid < TMB + 2) {
-        const int p = p0 - 1 + tid;
-        TT[tid] = (p >= 0 && p < T) ? pos_to_tb(p, n, d) : -1;
+// time index of LDS row L of the tile starting at p0, or -1 for a zero row
+template <bool MASKED>
+__device__ __forceinline__ int row_time(int L, int p0, const Layout& ly, int T, int n, int d) {
+    const int s = L / (ly.M + 2), k = L - s * (ly.M + 2);
+    if (ly.M == TMB) {
+        const int p = p0 - 1 + k;
+        if (p < 0 || p >= T) return -1;
+        if (!MASKED) {   // halos belong to the tile's sub-sequence only
+            if (k == 0 && p0 % n == 0) return -1;
+            if (k == TMB + 1 && (p0 + TMB) % n == 0) return -1;
+        }
+        return pos_to_tb(p, n, d);
     }
+    if (k == 0 || k == ly.M + 1) return -1;
+    return pos_to_tb(p0 + s * ly.M + k - 1, n, d);
+}
+
+// Per-launch LDS tables (SEG layouts): row L -> time offset ROWM (relative to the tile's first
+// position inside its sub-sequence; PAD for a zero row) and sub-sequence offset ROWS;
+// column c -> LDS row RMAP.  The time of row L in a tile starting at p0 is then
+//   t = (m0 + ROWM[L]) * d + j0 + ROWS[L],  m0 = p0 % n, j0 = p0 / n (uniform scalars),
+// valid iff ROWM[L] != PAD and 0 <= m0 + ROWM[L] < n.
+__device__ __forceinline__ void build_tables(int* ROWM, int* ROWS, int* RMAP, const Layout& ly,
+                                             int tid) {
+    for (int L = tid; L < NRMAX; L += NTH) {
+        const int s = L / (ly.M + 2), k = L - s * (ly.M + 2);
+        if (L >= ly.nrows) { ROWM[L] = PAD; ROWS[L] = 0; continue; }
+        if (ly.M == TMB) { ROWM[L] = L - 1; ROWS[L] = 0; }
+        else { ROWM[L] = (k == 0 || k == ly.M + 1) ? PAD : k - 1; ROWS[L] = s; }
+    }
+    for (int c = tid; c < TMB; c += NTH) RMAP[c] = rowmap(c, ly);
+}
+
+template <bool MASKED>
+__device__ __forceinline__ int tile_row_time(int L, int p0, int m0, int j0, const int* ROWM,
+                                             const int* ROWS, const Layout& ly, int T, int n, int d) {
+    if (MASKED) return row_time<true>(L, p0, ly, T, n, d);
+    const int mo = ROWM[L];
+    const int m = m0 + mo;
+    return (mo != PAD && m >= 0 && m < n) ? m * d + j0 + ROWS[L] : -1;
+}
+
+__device__ __forceinline__ bool is_center(int L, const Layout& ly) {
+    const int k = L % (ly.M + 2);
+    return k >= 1 && k <= ly.M;
+}
+
+// e > 0 mask of one staged 256-B row, assembled by its 16 lanes (q = lane & 15); lane q=0
+// returns the 4 words (channels 0-31, 32-63, ...).
+__device__ __forceinline__ uint4 row_sign_bits(uint4 v, int q, int lane) {
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        bits |= ((short)(d[j] & 0xffffu) > 0 ? 1u : 0u) << (2 * j);
+        bits |= ((short)(d[j] >> 16) > 0 ? 1u : 0u) << (2 * j + 1);
+    }
+    uint32_t m = bits << (8 * (q & 3));
+    m |= (uint32_t)__shfl_xor((int)m, 1);
+    m |= (uint32_t)__shfl_xor((int)m, 2);
+    const uint32_t w1 = (uint32_t)__shfl((int)m, lane + 4);
+    const uint32_t w2 = (uint32_t)__shfl((int)m, lane + 8);
+    const uint32_t w3 = (uint32_t)__shfl((int)m, lane + 12);
+    return make_uint4(m, w1, w2, w3);
 }
 
 __device__ __forceinline__ void load_bias16(float (&bias)[16], const float* src, int h) {
@@ -72,77 +137,148 @@ __device__ __forceinline__ void load_bias16(float (&bias)[16], const float* src,
     }
 }
 
-// Persistent: grid = 2 workgroups per CU; each keeps its wave's 32 output channels of Wd^T
-// (3 taps x 128 k) and Wr^T as MFMA A fragments in registers for the whole launch and walks
-// tiles blockIdx.x, +gridDim.x, ...
-__global__ void __launch_bounds__(256, 2) k_block_fwd_bf16(FwdArgsB a) {
-    __shared__ __attribute__((aligned(16))) u16 X[(TMB + 2) * XSB];
-    __shared__ __attribute__((aligned(16))) u16 V[TMB * XSB];
+__device__ __forceinline__ uint4 add_bf16x8(uint4 a, uint4 b) {
+    return make_uint4(pack2(bflo(a.x) + bflo(b.x), bfhi(a.x) + bfhi(b.x)),
+                      pack2(bflo(a.y) + bflo(b.y), bfhi(a.y) + bfhi(b.y)),
+                      pack2(bflo(a.z) + bflo(b.z), bfhi(a.z) + bfhi(b.z)),
+                      pack2(bflo(a.w) + bflo(b.w), bfhi(a.w) + bfhi(b.w)));
+}
+
+template <bool MASKED>
+__global__ void __launch_bounds__(NTH, 1) k_block_fwd_bf16(FwdArgsB a, Layout ly) {
+    __shared__ __attribute__((aligned(16))) u16 X[NRMAX * XSB];   // raw e_l rows
+    __shared__ __attribute__((aligned(16))) u16 R[NRMAX * XSB];   // relu(e_l) rows
+    __shared__ __attribute__((aligned(16))) u16 V[TMB * XSB];     // relu(u) by column
     __shared__ __attribute__((aligned(16))) uint32_t MB[TMB * 4];
-    __shared__ int TT[TMB + 2];
+    __shared__ __attribute__((aligned(16))) u16 WR[C * XSB];      // Wr^T [co2][co] (1x1 A operand)
+    __shared__ int TTb[2][NRMAX];   // time index per LDS row (current / prefetched tile)
+    __shared__ int ROWM[NRMAX], ROWS[NRMAX], RMAP[TMB];
+    __shared__ __attribute__((aligned(16))) float BIAS[2 * C];      // b_d, b_r
     const int tiles = a.T / TMB;
     const int ntiles = a.B * tiles;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int co0 = w * 32;
+    const int cb = (w & 3) * 32;          // output-channel block
+    const int nh = w >> 2;                // column group: columns 32*NJ*nh ..
 
-    uint4 wd[3][8], wr[8];
+    uint4 wd[3][8];
 #pragma unroll
     for (int tp = 0; tp < 3; ++tp)
 #pragma unroll
         for (int kb = 0; kb < 8; ++kb)
-            wd[tp][kb] = *reinterpret_cast<const uint4*>(a.wdT + (size_t)tp * C * C + (size_t)(co0 + r) * C + 8 * h + kb * 16);
-#pragma unroll
-    for (int kb = 0; kb < 8; ++kb)
-        wr[kb] = *reinterpret_cast<const uint4*>(a.wrT + (size_t)(co0 + r) * C + 8 * h + kb * 16);
+            wd[tp][kb] = *reinterpret_cast<const uint4*>(a.wdT + (size_t)tp * C * C + (size_t)(cb + r) * C + 8 * h + kb * 16);
+    for (int i = tid; i < C * 16; i += NTH)
+        *reinterpret_cast<uint4*>(&WR[(i >> 4) * XSB + (i & 15) * 8]) =
+            *reinterpret_cast<const uint4*>(a.wrT + (size_t)(i >> 4) * C + (i & 15) * 8);
+    if (tid < C) { BIAS[tid] = a.bd[tid]; BIAS[C + tid] = a.br[tid]; }
+    build_tables(ROWM, ROWS, RMAP, ly, tid);
+    __syncthreads();
 
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // prefetch registers: piece j of this thread = LDS row (tid + j*NTH) >> 4, 16 B at q*8
+    uint4 pf[PF_K];
+    auto prefetch = [&](int tile, int* TTn) {
+        if (tile >= ntiles) return;
+        const int b = tile / tiles, p0 = (tile - b * tiles) * TMB;
+        const int m0 = p0 % a.n, j0 = p0 / a.n;
+        const u16* src = a.ein + (size_t)b * a.T * C;
+#pragma unroll
+        for (int j = 0; j < PF_K; ++j) {
+            const int i = tid + j * NTH;
+            const int L = i >> 4;
+            pf[j] = make_uint4(0, 0, 0, 0);
+            if (L < ly.nrows) {
+                const int t = tile_row_time<MASKED>(L, p0, m0, j0, ROWM, ROWS, ly, a.T, a.n, a.d);
+                if ((i & 15) == 0) TTn[L] = t;
+                if (t >= 0) pf[j] = *reinterpret_cast<const uint4*>(src + (uint32_t)(t * C + (i & 15) * 8));
+            }
+        }
+    };
+    prefetch(blockIdx.x, TTb[0]);
+    int it = 0;
+    STAMP_DECL
+
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
         const int b = tile / tiles;
         const int p0 = (tile - b * tiles) * TMB;
-        const size_t cb = (size_t)b * a.T * C;
+        const size_t cbase = (size_t)b * a.T * C;
         const size_t mbase = (size_t)b * a.T * 4;
-        __syncthreads();                       // previous tile's LDS fully consumed
-        tile_times(TT, p0, a.T, a.n, a.d, tid);
-        __syncthreads();
-        stage_rows(X, TT, a.ein, cb, a.me, mbase, tid);
-        __syncthreads();
-
-        bool ok0[4], ok2[4];
+        int* TT = TTb[it & 1];
+        uint32_t* meb = a.me + mbase;
+        STAMP(0)
+        __syncthreads();                                   // (A) previous tile consumed
+        STAMP(1)
+        // commit the prefetched rows (no global stores here: the prefetch that follows
+        // must not queue behind them)
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            const int m = (p0 + nt * 32 + r) % a.n;
-            ok0[nt] = m > 0;
-            ok2[nt] = m < a.n - 1;
+        for (int j = 0; j < PF_K; ++j) {
+            const int i = tid + j * NTH;
+            const int L = i >> 4, q = i & 15;
+            if (L >= ly.nrows) break;
+            *reinterpret_cast<uint4*>(&X[L * XSB + q * 8]) = pf[j];
+            *reinterpret_cast<uint4*>(&R[L * XSB + q * 8]) = relu8(pf[j]);
         }
-        // GEMM 1: u^T[co][row] = sum_{tap, ci} Wd[tap][ci][co] relu(e)[row + tap - 1][ci]
-        // (two passes of two 32-row N-tiles keep the accumulators at 32 VGPRs)
+        STAMP(2)
+        prefetch(tile + gridDim.x, TTb[(it + 1) & 1]);     // in flight during this tile
+        STAMP(3)
+        __syncthreads();                                   // (B)
+        STAMP(4)
+
+        int Lc[NJ];
+        bool ok0[NJ], ok2[NJ];
 #pragma unroll
-        for (int np = 0; np < 2; ++np) {
-            f32x16 acc[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
-#pragma unroll
-            for (int tp = 0; tp < 3; ++tp) {
-#pragma unroll
-                for (int kb = 0; kb < 8; ++kb) {
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const int nt = 2 * np + j;
-                        uint4 bv = *reinterpret_cast<const uint4*>(&X[(nt * 32 + r + tp) * XSB + kb * 16 + 8 * h]);
-                        bv = relu8(bv);
-                        const bool ok = tp == 0 ? ok0[nt] : (tp == 2 ? ok2[nt] : true);
-                        if (!ok) bv = make_uint4(0, 0, 0, 0);
-                        acc[j] = mfma_bf16(wd[tp][kb], bv, acc[j]);
-                    }
-                }
+        for (int j = 0; j < NJ; ++j) {
+            const int c = (NJ * nh + j) * 32 + r;
+            Lc[j] = RMAP[c];
+            ok0[j] = ok2[j] = true;
+            if (MASKED) {
+                const int m = (p0 + c) % a.n;
+                ok0[j] = m > 0;
+                ok2[j] = m < a.n - 1;
             }
-            // epilogue 1: + bias (masked.py:155), relu (model.py:107) -> V (bf16); u>0 bits
-            float bias[16];
-            load_bias16(bias, a.bd + co0, h);
+        }
+        // GEMM 1: u^T[co][c] = sum_{tap, ci} Wd[tap][ci][co] relu(e)[c + tap - 1][ci]
+        // 24 (tap, k-block) steps, B fragments fetched one step ahead of their MFMAs
+        f32x16 acc[NJ];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int row = (2 * np + j) * 32 + r;
+        for (int j = 0; j < NJ; ++j)
+            for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+        {
+            uint4 bcur[NJ], bnxt[NJ];
+            const u16* rb[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                rb[j] = &R[(Lc[j] - 1) * XSB + 8 * h];          // tap 0 row; taps 1, 2 follow
+                bcur[j] = *reinterpret_cast<const uint4*>(rb[j]);
+            }
+#pragma unroll
+            for (int st = 0; st < 24; ++st) {
+                const int tp = st >> 3, kb = st & 7;
+                if (st + 1 < 24) {
+                    const int tn = (st + 1) >> 3, kn = (st + 1) & 7;
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j)
+                        bnxt[j] = *reinterpret_cast<const uint4*>(rb[j] + tn * XSB + kn * 16);
+                }
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    uint4 bv = bcur[j];
+                    if (MASKED) {
+                        const bool ok = tp == 0 ? ok0[j] : (tp == 2 ? ok2[j] : true);
+                        if (!ok) bv = make_uint4(0, 0, 0, 0);
+                    }
+                    acc[j] = mfma_bf16(wd[tp][kb], bv, acc[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) bcur[j] = bnxt[j];
+            }
+        }
+        STAMP(5)
+        {   // epilogue 1: + bias (masked.py:155), relu (model.py:107) -> V; u>0 bits -> MB
+            float bias[16];
+            load_bias16(bias, BIAS + cb, h);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int c = (NJ * nh + j) * 32 + r;
                 uint32_t part = 0;
                 float v[16];
 #pragma unroll
@@ -152,42 +288,53 @@ __global__ void __launch_bounds__(256, 2) k_block_fwd_bf16(FwdArgsB a) {
                     v[i] = fmaxf(u, 0.f);
                 }
                 const uint32_t word = part | (uint32_t)__shfl_xor((int)part, 32);
-                if (h == 0) MB[row * 4 + w] = word;
+                if (h == 0) MB[c * 4 + (w & 3)] = word;
 #pragma unroll
                 for (int g = 0; g < 4; ++g)
-                    *reinterpret_cast<uint2*>(&V[row * XSB + co0 + 8 * g + 4 * h]) =
+                    *reinterpret_cast<uint2*>(&V[c * XSB + cb + 8 * g + 4 * h]) =
                         make_uint2(pack2(v[4 * g], v[4 * g + 1]), pack2(v[4 * g + 2], v[4 * g + 3]));
             }
         }
-        __syncthreads();
+        STAMP(6)
+        __syncthreads();                                   // (C)
+        STAMP(7)
         if (tid < TMB)
-            *reinterpret_cast<uint4*>(a.mu + mbase + (size_t)TT[tid + 1] * 4) =
+            *reinterpret_cast<uint4*>(a.mu + mbase + (uint32_t)(TT[RMAP[tid]] * 4)) =
                 *reinterpret_cast<const uint4*>(&MB[tid * 4]);
-
-        // GEMM 2: y^T[co2][row] = sum_co Wr[co][co2] v[row][co]   (model.py:109-114)
+        // GEMM 2: y^T[co2][c] = sum_co Wr[co][co2] v[c][co]   (model.py:109-114)
 #pragma unroll
-        for (int np = 0; np < 2; ++np) {
-            f32x16 acc[2];
+        for (int j = 0; j < NJ; ++j)
+            for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+        {
+            uint4 acur, anxt, bcur[NJ], bnxt[NJ];
+            acur = *reinterpret_cast<const uint4*>(&WR[(cb + r) * XSB + 8 * h]);
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-                for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+            for (int j = 0; j < NJ; ++j)
+                bcur[j] = *reinterpret_cast<const uint4*>(&V[((NJ * nh + j) * 32 + r) * XSB + 8 * h]);
 #pragma unroll
             for (int kb = 0; kb < 8; ++kb) {
+                if (kb + 1 < 8) {
+                    anxt = *reinterpret_cast<const uint4*>(&WR[(cb + r) * XSB + (kb + 1) * 16 + 8 * h]);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const uint4 bv = *reinterpret_cast<const uint4*>(&V[((2 * np + j) * 32 + r) * XSB + kb * 16 + 8 * h]);
-                    acc[j] = mfma_bf16(wr[kb], bv, acc[j]);
+                    for (int j = 0; j < NJ; ++j)
+                        bnxt[j] = *reinterpret_cast<const uint4*>(&V[((NJ * nh + j) * 32 + r) * XSB + (kb + 1) * 16 + 8 * h]);
                 }
-            }
-            // epilogue 2: e_{l+1} = e_l + (y + b_r), written over this wave's columns of X
-            float bias[16];
-            load_bias16(bias, a.br + co0, h);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int row = (2 * np + j) * 32 + r;
+                for (int j = 0; j < NJ; ++j) acc[j] = mfma_bf16(acur, bcur[j], acc[j]);
+                acur = anxt;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) bcur[j] = bnxt[j];
+            }
+        }
+        STAMP(8)
+        {   // epilogue 2: e_{l+1} = e_l + (y + b_r), over this wave's channels of X in place
+            float bias[16];
+            load_bias16(bias, BIAS + C + cb, h);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    uint2* px = reinterpret_cast<uint2*>(&X[(row + 1) * XSB + co0 + 8 * g + 4 * h]);
+                    uint2* px = reinterpret_cast<uint2*>(&X[Lc[j] * XSB + cb + 8 * g + 4 * h]);
                     const uint2 ev = *px;
                     const float o0 = bflo(ev.x) + (acc[j][4 * g + 0] + bias[4 * g + 0]);
                     const float o1 = bfhi(ev.x) + (acc[j][4 * g + 1] + bias[4 * g + 1]);
@@ -197,180 +344,249 @@ __global__ void __launch_bounds__(256, 2) k_block_fwd_bf16(FwdArgsB a) {
                 }
             }
         }
-        __syncthreads();
-        for (int i = tid; i < TMB * 16; i += 256) {
-            const int rr = i >> 4, q = i & 15;
-            *reinterpret_cast<uint4*>(a.eout + cb + (size_t)TT[rr + 1] * C + q * 8) =
-                *reinterpret_cast<const uint4*>(&X[(rr + 1) * XSB + q * 8]);
+        STAMP(9)
+        __syncthreads();                                   // (D)
+        STAMP(10)
+        // write e_{l+1} rows; the e_l > 0 mask (== relu(e_l) != 0, from R) leaves with them
+        u16* dst = a.eout + cbase;
+#pragma unroll
+        for (int j = 0; j < TMB * 16 / NTH; ++j) {
+            const int i = tid + j * NTH;
+            const int L = RMAP[i >> 4], q = i & 15;
+            const int t = TT[L];
+            *reinterpret_cast<uint4*>(dst + (uint32_t)(t * C + q * 8)) =
+                *reinterpret_cast<const uint4*>(&X[L * XSB + q * 8]);
+            const uint4 mw = row_sign_bits(*reinterpret_cast<const uint4*>(&R[L * XSB + q * 8]), q, lane);
+            if (q == 0) *reinterpret_cast<uint4*>(meb + (uint32_t)(t * 4)) = mw;
         }
+        STAMP(11)
     }
+    STAMP_FLUSH(a.stamps)
 }
 
-__global__ void __launch_bounds__(256, 2) k_block_bwd_bf16(BwdArgsB a) {
-    __shared__ __attribute__((aligned(16))) u16 G[(TMB + 2) * XSB];
-    __shared__ __attribute__((aligned(16))) u16 U[(TMB + 2) * XSB];
-    __shared__ __attribute__((aligned(16))) uint32_t MU[(TMB + 2) * 4];
-    __shared__ __attribute__((aligned(16))) uint32_t ME[TMB * 4];
-    __shared__ int TT[TMB + 2];
+template <bool MASKED>
+__global__ void __launch_bounds__(NTH, 1) k_block_bwd_bf16(BwdArgsB a, Layout ly) {
+    __shared__ __attribute__((aligned(16))) u16 G[NRMAX * XSB];   // tot = g_{l+1} + D_{l+1}
+    __shared__ __attribute__((aligned(16))) u16 U[NRMAX * XSB];   // g_u rows
+    __shared__ __attribute__((aligned(16))) uint32_t MU[NRMAX * 4];
+    __shared__ __attribute__((aligned(16))) uint32_t ME[NRMAX * 4];
+    __shared__ __attribute__((aligned(16))) u16 WR[C * XSB];      // Wr [i][o] (step-1 A operand)
+    __shared__ int TTb[2][NRMAX];   // time index per LDS row (current / prefetched tile)
+    __shared__ int ROWM[NRMAX], ROWS[NRMAX], RMAP[TMB];
     const int tiles = a.T / TMB;
     const int ntiles = a.B * tiles;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int c0 = w * 32;
+    const int cb = (w & 3) * 32;
+    const int nh = w >> 2;                // column group: columns 32*NJ*nh ..
 
-    uint4 wr[8], wd[3][8];
-#pragma unroll
-    for (int kb = 0; kb < 8; ++kb)
-        wr[kb] = *reinterpret_cast<const uint4*>(a.wr + (size_t)(c0 + r) * C + 8 * h + kb * 16);
+    uint4 wd[3][8];
+    for (int i = tid; i < C * 16; i += NTH)
+        *reinterpret_cast<uint4*>(&WR[(i >> 4) * XSB + (i & 15) * 8]) =
+            *reinterpret_cast<const uint4*>(a.wr + (size_t)(i >> 4) * C + (i & 15) * 8);
 #pragma unroll
     for (int tp = 0; tp < 3; ++tp)
 #pragma unroll
         for (int kb = 0; kb < 8; ++kb)
-            wd[tp][kb] = *reinterpret_cast<const uint4*>(a.wd + (size_t)tp * C * C + (size_t)(c0 + r) * C + 8 * h + kb * 16);
+            wd[tp][kb] = *reinterpret_cast<const uint4*>(a.wd + (size_t)tp * C * C + (size_t)(cb + r) * C + 8 * h + kb * 16);
 
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // pad rows of U are never written by a tile: zero the whole image once
+    for (int i = tid; i < NRMAX * XSB / 8; i += NTH) reinterpret_cast<uint4*>(U)[i] = make_uint4(0, 0, 0, 0);
+    build_tables(ROWM, ROWS, RMAP, ly, tid);
+    __syncthreads();
+
+    uint4 pg[PF_K], pd[PF_K];
+    uint4 pmu = make_uint4(0, 0, 0, 0), pme = make_uint4(0, 0, 0, 0);
+    auto prefetch = [&](int tile, int* TTn) {
+        if (tile >= ntiles) return;
+        const int b = tile / tiles, p0 = (tile - b * tiles) * TMB;
+        const int m0 = p0 % a.n, j0 = p0 / a.n;
+        const size_t cbase = (size_t)b * a.T * C;
+        const u16* gsrc = a.gin ? a.gin + cbase : nullptr;
+        const u16* dsrc = a.din ? a.din + cbase : nullptr;
+#pragma unroll
+        for (int j = 0; j < PF_K; ++j) {
+            const int i = tid + j * NTH;
+            const int L = i >> 4;
+            pg[j] = make_uint4(0, 0, 0, 0);
+            pd[j] = make_uint4(0, 0, 0, 0);
+            if (L < ly.nrows) {
+                const int t = tile_row_time<MASKED>(L, p0, m0, j0, ROWM, ROWS, ly, a.T, a.n, a.d);
+                if ((i & 15) == 0) TTn[L] = t;
+                if (t >= 0) {
+                    const uint32_t o = (uint32_t)(t * C + (i & 15) * 8);
+                    if (gsrc) pg[j] = *reinterpret_cast<const uint4*>(gsrc + o);
+                    if (dsrc) pd[j] = *reinterpret_cast<const uint4*>(dsrc + o);
+                }
+            }
+        }
+        pmu = make_uint4(0, 0, 0, 0);
+        pme = make_uint4(0, 0, 0, 0);
+        if (tid < ly.nrows) {
+            const int t = tile_row_time<MASKED>(tid, p0, m0, j0, ROWM, ROWS, ly, a.T, a.n, a.d);
+            if (t >= 0) {
+                const size_t mbase = (size_t)b * a.T * 4;
+                pmu = *reinterpret_cast<const uint4*>(a.mu + mbase + (uint32_t)(t * 4));
+                pme = *reinterpret_cast<const uint4*>(a.me + mbase + (uint32_t)(t * 4));
+            }
+        }
+    };
+    prefetch(blockIdx.x, TTb[0]);
+    int it = 0;
+
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
         const int b = tile / tiles;
         const int p0 = (tile - b * tiles) * TMB;
-        const size_t cb = (size_t)b * a.T * C;
-        const size_t mbase = (size_t)b * a.T * 4;
-        __syncthreads();
-        tile_times(TT, p0, a.T, a.n, a.d, tid);
-        __syncthreads();
-        // tot = g_{l+1} + D_{l+1}
-        for (int i = tid; i < (TMB + 2) * 16; i += 256) {
-            const int rr = i >> 4, q = i & 15;
-            const int t = TT[rr];
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (t >= 0) {
-                const size_t o = cb + (size_t)t * C + q * 8;
-                if (a.gin && a.din) {
-                    const uint4 g4 = *reinterpret_cast<const uint4*>(a.gin + o);
-                    const uint4 d4 = *reinterpret_cast<const uint4*>(a.din + o);
-                    v.x = pack2(bflo(g4.x) + bflo(d4.x), bfhi(g4.x) + bfhi(d4.x));
-                    v.y = pack2(bflo(g4.y) + bflo(d4.y), bfhi(g4.y) + bfhi(d4.y));
-                    v.z = pack2(bflo(g4.z) + bflo(d4.z), bfhi(g4.z) + bfhi(d4.z));
-                    v.w = pack2(bflo(g4.w) + bflo(d4.w), bfhi(g4.w) + bfhi(d4.w));
-                } else if (a.gin) {
-                    v = *reinterpret_cast<const uint4*>(a.gin + o);
-                } else if (a.din) {
-                    v = *reinterpret_cast<const uint4*>(a.din + o);
-                }
-            }
-            *reinterpret_cast<uint4*>(&G[rr * XSB + q * 8]) = v;
+        const size_t cbase = (size_t)b * a.T * C;
+        int* TT = TTb[it & 1];
+        __syncthreads();                                   // (A)
+#pragma unroll
+        for (int j = 0; j < PF_K; ++j) {
+            const int i = tid + j * NTH;
+            const int L = i >> 4, q = i & 15;
+            if (L >= ly.nrows) break;
+            const uint4 v = (a.gin && a.din) ? add_bf16x8(pg[j], pd[j]) : (a.gin ? pg[j] : pd[j]);
+            *reinterpret_cast<uint4*>(&G[L * XSB + q * 8]) = v;
         }
-        if (tid < TMB + 2) {
-            const int t = TT[tid];
-            uint4 mw = make_uint4(0, 0, 0, 0);
-            if (t >= 0) mw = *reinterpret_cast<const uint4*>(a.mu + mbase + (size_t)t * 4);
-            *reinterpret_cast<uint4*>(&MU[tid * 4]) = mw;
-            if (tid < TMB)
-                *reinterpret_cast<uint4*>(&ME[tid * 4]) =
-                    *reinterpret_cast<const uint4*>(a.me + mbase + (size_t)TT[tid + 1] * 4);
+        if (tid < ly.nrows) {
+            *reinterpret_cast<uint4*>(&MU[tid * 4]) = pmu;
+            *reinterpret_cast<uint4*>(&ME[tid * 4]) = pme;
         }
-        __syncthreads();
+        prefetch(tile + gridDim.x, TTb[(it + 1) & 1]);
+        __syncthreads();                                   // (B)
 
-        bool ok0[4], ok2[4];
+        int Lc[NJ];
+        bool ok0[NJ], ok2[NJ];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            const int m = (p0 + nt * 32 + r) % a.n;
-            ok0[nt] = m > 0;
-            ok2[nt] = m < a.n - 1;
+        for (int j = 0; j < NJ; ++j) {
+            const int c = (NJ * nh + j) * 32 + r;
+            Lc[j] = RMAP[c];
+            ok0[j] = ok2[j] = true;
+            if (MASKED) {
+                const int m = (p0 + c) % a.n;
+                ok0[j] = m > 0;
+                ok2[j] = m < a.n - 1;
+            }
         }
-        // step 1: g_v^T[i][row] = sum_o Wr[i][o] tot[row][o];  g_u = [u>0] g_v -> U
+        // step 1: g_v^T[i][c] = sum_o Wr[i][o] tot[c][o];  g_u = [u>0] g_v -> U
+        f32x16 acc[NJ];
 #pragma unroll
-        for (int np = 0; np < 2; ++np) {
-            f32x16 acc[2];
+        for (int j = 0; j < NJ; ++j)
+            for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+        {
+            uint4 acur, anxt, bcur[NJ], bnxt[NJ];
+            acur = *reinterpret_cast<const uint4*>(&WR[(cb + r) * XSB + 8 * h]);
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-                for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+            for (int j = 0; j < NJ; ++j) bcur[j] = *reinterpret_cast<const uint4*>(&G[Lc[j] * XSB + 8 * h]);
 #pragma unroll
             for (int kb = 0; kb < 8; ++kb) {
+                if (kb + 1 < 8) {
+                    anxt = *reinterpret_cast<const uint4*>(&WR[(cb + r) * XSB + (kb + 1) * 16 + 8 * h]);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const uint4 bv = *reinterpret_cast<const uint4*>(&G[((2 * np + j) * 32 + r + 1) * XSB + kb * 16 + 8 * h]);
-                    acc[j] = mfma_bf16(wr[kb], bv, acc[j]);
+                    for (int j = 0; j < NJ; ++j)
+                        bnxt[j] = *reinterpret_cast<const uint4*>(&G[Lc[j] * XSB + (kb + 1) * 16 + 8 * h]);
                 }
-            }
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int row = (2 * np + j) * 32 + r;
-                const uint32_t mw = MU[(row + 1) * 4 + w];
-                float v[16];
+                for (int j = 0; j < NJ; ++j) acc[j] = mfma_bf16(acur, bcur[j], acc[j]);
+                acur = anxt;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] = ((mw >> acc_row(i, h)) & 1u) ? acc[j][i] : 0.f;
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    *reinterpret_cast<uint2*>(&U[(row + 1) * XSB + c0 + 8 * g + 4 * h]) =
-                        make_uint2(pack2(v[4 * g], v[4 * g + 1]), pack2(v[4 * g + 2], v[4 * g + 3]));
+                for (int j = 0; j < NJ; ++j) bcur[j] = bnxt[j];
             }
         }
-        {   // the two halo rows (LDS rows 0 and TMB+1) as one more 32-column MFMA tile:
-            // column r computes halo row (r & 1); lanes r = 0, 1 keep their results.
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const uint32_t mw = MU[Lc[j] * 4 + (w & 3)];
+            float v[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = ((mw >> acc_row(i, h)) & 1u) ? acc[j][i] : 0.f;
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                *reinterpret_cast<uint2*>(&U[Lc[j] * XSB + cb + 8 * g + 4 * h]) =
+                    make_uint2(pack2(v[4 * g], v[4 * g + 1]), pack2(v[4 * g + 2], v[4 * g + 3]));
+        }
+        if (ly.M == TMB && nh == 0) {
+            // halo rows 0 and TMB+1 (neighbour taps of the edge columns) as one more tile:
+            // column r computes halo (r & 1); lanes r = 0, 1 keep their results
             const int hrow = (r & 1) ? TMB + 1 : 0;
             f32x16 hacc;
             for (int i = 0; i < 16; ++i) hacc[i] = 0.f;
 #pragma unroll
             for (int kb = 0; kb < 8; ++kb) {
+                const uint4 av = *reinterpret_cast<const uint4*>(&WR[(cb + r) * XSB + kb * 16 + 8 * h]);
                 const uint4 bv = *reinterpret_cast<const uint4*>(&G[hrow * XSB + kb * 16 + 8 * h]);
-                hacc = mfma_bf16(wr[kb], bv, hacc);
+                hacc = mfma_bf16(av, bv, hacc);
             }
             if (r < 2) {
-                const uint32_t mw = TT[hrow] >= 0 ? MU[hrow * 4 + w] : 0u;
+                const uint32_t mw = TT[hrow] >= 0 ? MU[hrow * 4 + (w & 3)] : 0u;
                 float v[16];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) v[i] = ((mw >> acc_row(i, h)) & 1u) ? hacc[i] : 0.f;
 #pragma unroll
                 for (int g = 0; g < 4; ++g)
-                    *reinterpret_cast<uint2*>(&U[hrow * XSB + c0 + 8 * g + 4 * h]) =
+                    *reinterpret_cast<uint2*>(&U[hrow * XSB + cb + 8 * g + 4 * h]) =
                         make_uint2(pack2(v[4 * g], v[4 * g + 1]), pack2(v[4 * g + 2], v[4 * g + 3]));
             }
         }
-        __syncthreads();
+        __syncthreads();                                   // (C)
 
-        // step 2: gh^T[ci][row] = sum_{tap, co} Wd[tap][ci][co] g_u[row - tap + 1][co]
+        // step 2: gh^T[ci][c] = sum_{tap, co} Wd[tap][ci][co] g_u[c - tap + 1][co]
 #pragma unroll
-        for (int np = 0; np < 2; ++np) {
-            f32x16 acc[2];
+        for (int j = 0; j < NJ; ++j)
+            for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+        {
+            uint4 bcur[NJ], bnxt[NJ];
+            const u16* ub[NJ];
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-                for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
-#pragma unroll
-            for (int tp = 0; tp < 3; ++tp) {
-#pragma unroll
-                for (int kb = 0; kb < 8; ++kb) {
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const int nt = 2 * np + j;
-                        uint4 bv = *reinterpret_cast<const uint4*>(&U[(nt * 32 + r + 2 - tp) * XSB + kb * 16 + 8 * h]);
-                        const bool ok = tp == 0 ? ok2[nt] : (tp == 2 ? ok0[nt] : true);
-                        if (!ok) bv = make_uint4(0, 0, 0, 0);
-                        acc[j] = mfma_bf16(wd[tp][kb], bv, acc[j]);
-                    }
-                }
+            for (int j = 0; j < NJ; ++j) {
+                ub[j] = &U[(Lc[j] - 1) * XSB + 8 * h];          // tap 2 row; taps 1, 0 follow
+                bcur[j] = *reinterpret_cast<const uint4*>(ub[j] + 2 * XSB);
             }
-            // epilogue: g_l = tot + [e_l > 0] gh, over this wave's columns of G (centre rows)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int row = (2 * np + j) * 32 + r;
-                const uint32_t mw = ME[row * 4 + w];
+            for (int st = 0; st < 24; ++st) {
+                const int tp = st >> 3, kb = st & 7;
+                if (st + 1 < 24) {
+                    const int tn = (st + 1) >> 3, kn = (st + 1) & 7;
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    uint2* pg = reinterpret_cast<uint2*>(&G[(row + 1) * XSB + c0 + 8 * g + 4 * h]);
-                    const uint2 tv = *pg;
-                    const int R = 8 * g + 4 * h;
-                    const float o0 = bflo(tv.x) + (((mw >> (R + 0)) & 1u) ? acc[j][4 * g + 0] : 0.f);
-                    const float o1 = bfhi(tv.x) + (((mw >> (R + 1)) & 1u) ? acc[j][4 * g + 1] : 0.f);
-                    const float o2 = bflo(tv.y) + (((mw >> (R + 2)) & 1u) ? acc[j][4 * g + 2] : 0.f);
-                    const float o3 = bfhi(tv.y) + (((mw >> (R + 3)) & 1u) ? acc[j][4 * g + 3] : 0.f);
-                    *pg = make_uint2(pack2(o0, o1), pack2(o2, o3));
+                    for (int j = 0; j < NJ; ++j)
+                        bnxt[j] = *reinterpret_cast<const uint4*>(ub[j] + (2 - tn) * XSB + kn * 16);
                 }
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    uint4 bv = bcur[j];
+                    if (MASKED) {
+                        const bool ok = tp == 0 ? ok2[j] : (tp == 2 ? ok0[j] : true);
+                        if (!ok) bv = make_uint4(0, 0, 0, 0);
+                    }
+                    acc[j] = mfma_bf16(wd[tp][kb], bv, acc[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) bcur[j] = bnxt[j];
             }
         }
-        __syncthreads();
-        for (int i = tid; i < TMB * 16; i += 256) {
-            const int rr = i >> 4, q = i & 15;
-            *reinterpret_cast<uint4*>(a.gout + cb + (size_t)TT[rr + 1] * C + q * 8) =
-                *reinterpret_cast<const uint4*>(&G[(rr + 1) * XSB + q * 8]);
+        // epilogue: g_l = tot + [e_l > 0] gh, over this wave's channels of G in place
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const uint32_t mw = ME[Lc[j] * 4 + (w & 3)];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                uint2* pgp = reinterpret_cast<uint2*>(&G[Lc[j] * XSB + cb + 8 * g + 4 * h]);
+                const uint2 tv = *pgp;
+                const int Rr = 8 * g + 4 * h;
+                const float o0 = bflo(tv.x) + (((mw >> (Rr + 0)) & 1u) ? acc[j][4 * g + 0] : 0.f);
+                const float o1 = bfhi(tv.x) + (((mw >> (Rr + 1)) & 1u) ? acc[j][4 * g + 1] : 0.f);
+                const float o2 = bflo(tv.y) + (((mw >> (Rr + 2)) & 1u) ? acc[j][4 * g + 2] : 0.f);
+                const float o3 = bfhi(tv.y) + (((mw >> (Rr + 3)) & 1u) ? acc[j][4 * g + 3] : 0.f);
+                *pgp = make_uint2(pack2(o0, o1), pack2(o2, o3));
+            }
+        }
+        __syncthreads();                                   // (D)
+        u16* dst = a.gout + cbase;
+#pragma unroll
+        for (int j = 0; j < TMB * 16 / NTH; ++j) {
+            const int i = tid + j * NTH;
+            const int L = RMAP[i >> 4], q = i & 15;
+            *reinterpret_cast<uint4*>(dst + (uint32_t)(TT[L] * C + q * 8)) =
+                *reinterpret_cast<const uint4*>(&G[L * XSB + q * 8]);
         }
     }
 }
@@ -386,13 +602,28 @@ static int num_cus() {
     return g_cus;
 }
 
+// Segment layout when every tile holds whole sub-sequences of >= 32 positions or lies inside
+// one; otherwise one segment with halos and per-column tap masks.
+static bool pick_layout(int n, Layout& ly) {
+    if (n % TMB == 0) { ly.M = TMB; ly.nrows = TMB + 2; return false; }
+    if (n < TMB && TMB % n == 0 && n >= 32) { ly.M = n; ly.nrows = (TMB / n) * (n + 2); return false; }
+    ly.M = TMB; ly.nrows = TMB + 2;
+    return true;
+}
+
 void launch_block_fwd_bf16(const FwdArgsB& a, hipStream_t s) {
     const int nt = a.B * (a.T / TMB);
-    hipLaunchKernelGGL(k_block_fwd_bf16, dim3(std::min(nt, 2 * num_cus())), dim3(256), 0, s, a);
+    const dim3 grid(std::min(nt, num_cus()));
+    Layout ly;
+    if (pick_layout(a.n, ly)) hipLaunchKernelGGL(k_block_fwd_bf16<true>, grid, dim3(NTH), 0, s, a, ly);
+    else hipLaunchKernelGGL(k_block_fwd_bf16<false>, grid, dim3(NTH), 0, s, a, ly);
 }
 void launch_block_bwd_bf16(const BwdArgsB& a, hipStream_t s) {
     const int nt = a.B * (a.T / TMB);
-    hipLaunchKernelGGL(k_block_bwd_bf16, dim3(std::min(nt, 2 * num_cus())), dim3(256), 0, s, a);
+    const dim3 grid(std::min(nt, num_cus()));
+    Layout ly;
+    if (pick_layout(a.n, ly)) hipLaunchKernelGGL(k_block_bwd_bf16<true>, grid, dim3(NTH), 0, s, a, ly);
+    else hipLaunchKernelGGL(k_block_bwd_bf16<false>, grid, dim3(NTH), 0, s, a, ly);
 }
 
 }  // namespace ast

@@ -193,7 +193,7 @@ def main():
     gram_fwd_ms = tm['gram_fwd_ms'] / calls
     gram_bwd_ms = tm['gram_bwd_ms'] / calls
     L = len(style_ids)
-    gram_bytes = L * B * T * 128 * 4.0
+    gram_bytes = L * B * T * 128 * (4.0 if args.precision == 'fp32' else 2.0)
     out = {
         'metric': 'style-transfer iters/sec, 256x16384-sample batch, 30-layer WaveNet encoder',
         'value': value, 'unit': 'iters/s', 'n_gpus': ws, 'steps': args.steps,

@@ -1,0 +1,100 @@
+"""CPU: libastyle.so loads, exports every symbol include/astyle.h declares, its ast_cfg layout
+matches the header, and host-side validation (ast_workspace_bytes: no HIP calls) behaves."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from audio_style_transfer_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, 'include', 'astyle.h')
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(ast_[a-z_]+)\s*\(', src)))
+
+
+def test_header_and_binding_agree():
+    assert sorted(_lib.EXPORTS) == header_functions()
+
+
+def test_library_exports_every_header_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(['nm', '-D', '--defined-only', _lib.LIB_PATH], capture_output=True,
+                         text=True).stdout
+    for name in header_functions():
+        assert re.search(r'\bT %s\b' % name, out), name
+
+
+def test_cfg_struct_layout_matches_header(tmp_path):
+    c = tmp_path / 'probe.c'
+    c.write_text('#include "astyle.h"\n#include <stdio.h>\n#include <stddef.h>\n'
+                 'int main(){printf("%zu %zu %zu %zu\\n", sizeof(ast_cfg), '
+                 'offsetof(ast_cfg, style_ids), offsetof(ast_cfg, precision), '
+                 'offsetof(ast_cfg, lambd));return 0;}\n')
+    exe = tmp_path / 'probe'
+    subprocess.run(['gcc', '-I', os.path.join(ROOT, 'include'), str(c), '-o', str(exe)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    C = _lib.AstCfg
+    assert vals == [ctypes.sizeof(C), C.style_ids.offset, C.precision.offset, C.lambd.offset]
+
+
+def _cfg(**kw):
+    c = _lib.AstCfg()
+    c.batch, c.T = kw.get('batch', 2), kw.get('T', 16384)
+    cont = kw.get('cont', [29])
+    sty = kw.get('style', list(range(30)))
+    c.n_cont = len(cont)
+    for i, v in enumerate(cont):
+        c.cont_ids[i] = v
+    c.n_style = len(sty)
+    for i, v in enumerate(sty):
+        c.style_ids[i] = v
+    c.cnt_channels = kw.get('cnt', 128)
+    c.nb_channels = kw.get('nb', 128)
+    c.gatys = kw.get('gatys', 0)
+    c.precision = kw.get('precision', 0)
+    c.lambd = 100.0
+    return c
+
+
+def _ws(**kw):
+    lib = _lib.load()
+    n = ctypes.c_size_t()
+    rc = lib.ast_workspace_bytes(ctypes.byref(_cfg(**kw)), ctypes.byref(n))
+    return rc, n.value, lib.ast_last_error().decode()
+
+
+def test_workspace_scales_with_precision_and_blocks():
+    rc32, n32, _ = _ws(precision=0)
+    rc16, n16, _ = _ws(precision=1)
+    assert rc32 == 0 and rc16 == 0 and n16 < n32
+    # stack 0 + content 25 runs 26 blocks (TF prunes the rest)
+    rc, n26, _ = _ws(cont=[25], style=list(range(10)))
+    assert rc == 0 and n26 < n32
+
+
+@pytest.mark.parametrize('kw,msg', [
+    (dict(T=1000), 'multiple of 512'),
+    (dict(cont=[32]), 'content layer ids'),
+    (dict(style=[31]), 'style layer ids'),
+    (dict(precision=2), 'precision'),
+    (dict(cnt=0), 'cnt_channels'),
+])
+def test_invalid_configs_fail_loudly(kw, msg):
+    rc, _, err = _ws(**kw)
+    assert rc == -1 and msg in err, (rc, err)
+
+
+def test_engine_refuses_cpu_device():
+    torch = pytest.importorskip('torch')
+    from audio_style_transfer_amd.engine import StyleEngine
+    with pytest.raises(_lib.AstError):
+        StyleEngine(1, 512, [0], [0], device=torch.device('cpu'))
