@@ -1,0 +1,251 @@
+"""Drop-in for the reference's methods.py (CLI + GatysNet), running on libastyle.so.
+
+Same argparse surface (methods.py:243-269), same output layout (utils.gt_s_path / crt_t_fol,
+ori.wav, style.wav, ep-N.wav, gram/spectrogram PNGs), same optimisation protocol: per epoch one
+scipy L-BFGS-B minimize(maxiter=100) whose every function evaluation is one ast_loss_grad
+(ScipyOptimizerInterface, methods.py:132-137,167), early stop when an epoch used < 50
+evaluations (methods.py:180).  Additions: --optimizer adam (fused device Adam, many clips),
+--precision bf16, --weights (npz of TF-named encoder variables).
+
+The TF checkpoint itself cannot be read here (no TF): --ckpt_path is
+honoured when it points at an .npz of TF-named arrays; otherwise seeded synthetic weights
+are used and a warning is printed.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+import warnings
+
+import numpy as np
+import torch
+
+from . import utils
+from .engine import StyleEngine, resolve_style_ids
+from .weights import synthetic_weights
+
+
+def load_weights(path):
+    """TF-named encoder weights from an .npz (allow_pickle=False); None if unavailable."""
+    if path and os.path.isfile(path) and path.endswith('.npz'):
+        with np.load(path, allow_pickle=False) as z:
+            return {k: z[k] for k in z.files}
+    return None
+
+
+def stft_regularizer(x: torch.Tensor):
+    """methods.py:121-123: mean(abs(Re S) + abs(Im S)), S = stft(inv_mu_law(x), 1024, 512)
+    (periodic Hann, no padding), utils.abs/sign/inv_mu_law semantics (utils.py:92-104).
+    x: [B, T] (mu-law units) -> (value [B], d value / d x [B, T]) via autograd on the GPU."""
+    x = x.detach().requires_grad_(True)
+
+    def abs_tf(v):
+        return torch.clamp(v, min=1e-12) + torch.clamp(-v, min=0.0)
+
+    o = (x + 0.5) * 2.0 / 256.0
+    sgn = torch.where(o.abs() <= 1e-12, torch.zeros_like(o), o) / abs_tf(o)
+    a = sgn / 255.0 * (256.0 ** abs_tf(o) - 1)
+    a = torch.where(x == 0, x, a)
+    S = torch.stft(a, n_fft=1024, hop_length=512, win_length=1024,
+                   window=torch.hann_window(1024, periodic=True, device=x.device),
+                   center=False, return_complex=True)
+    reg = (abs_tf(S.real) + abs_tf(S.imag)).mean(dim=(-2, -1))
+    g, = torch.autograd.grad(reg.sum(), x)
+    return reg.detach(), g
+
+
+class GatysNet(object):
+    """methods.py:19-216, on one GPU; ``batch`` > 1 optimises independent clips together."""
+
+    def __init__(self, savepath='./data/out',
+                 checkpoint_path='./nsynth/model/wavenet-ckpt/model.ckpt-200000',
+                 logdir='./log', figdir='./data/fig', stack=0, batch_size=16384, sr=16000,
+                 cont_lyr_ids=[29], nb_channels=128, cnt_channels=128, gatys=False,
+                 style_lyr_ids=None, precision='fp32', device=None, weights=None, plots=True):
+        self.logdir = logdir
+        self.savepath = savepath
+        self.checkpoint_path = checkpoint_path
+        self.figdir = figdir
+        self.batch_size = batch_size
+        self.sr = sr
+        self.late = (batch_size - (batch_size // 4096) * 4000) // 2          # methods.py:39
+        self.cont_lyr_ids = list(cont_lyr_ids)
+        self.style_lyr_ids = resolve_style_ids(stack, style_lyr_ids)        # methods.py:60-66
+        self.nb_channels, self.cnt_channels, self.gatys = nb_channels, cnt_channels, gatys
+        self.precision = precision
+        self.device = device or torch.device('cuda', torch.cuda.current_device())
+        self.plots = plots
+        if weights is None:
+            weights = load_weights(checkpoint_path)
+            if weights is None:
+                warnings.warn('checkpoint %r not readable here (TF checkpoint reader not built); '
+                              'using seeded synthetic encoder weights' % checkpoint_path)
+                weights = synthetic_weights(0)
+        self.weights = weights
+        self.engine = self.build(batch_size)
+        self.embeds_shape = self.engine.style_shape
+
+    def build(self, length, batch=1, lambd=100.0):
+        """methods.py:44-77: encoder + taps + Gram + l2norm, here one libastyle context."""
+        return StyleEngine(batch, length, self.cont_lyr_ids, self.style_lyr_ids,
+                           cnt_channels=self.cnt_channels, nb_channels=self.nb_channels,
+                           gatys=self.gatys, lambd=lambd, precision=self.precision,
+                           device=self.device, weights=self.weights)
+
+    def get_embeds(self, aud, is_content=True):
+        """methods.py:86-95: mu-law encode the clip and fetch embeds_c or embeds_s."""
+        aud = np.asarray(aud)
+        if aud.ndim == 1:
+            aud = aud[:self.batch_size].reshape(1, self.batch_size)
+        x = torch.tensor(utils.mu_law_numpy(aud), dtype=torch.float32, device=self.device)
+        emb_c, emb_s = self.engine.embeds(x, content=is_content, style=not is_content)
+        return (emb_c if is_content else emb_s)[0].cpu().numpy()
+
+    def get_style_phi(self, filename, max_examples=5, show_mat=True):
+        """methods.py:97-111: mean style embedding over <= 5 consecutive clips."""
+        audio, _ = utils.load_audio(filename, sr=self.sr, audio_channel=0)
+        I = []
+        i = 0
+        while i + self.batch_size <= min(len(audio), max_examples * self.batch_size):
+            I.append(self.get_embeds(audio[i:i + self.batch_size], is_content=False))
+            i += self.batch_size
+        phi = np.mean(I, axis=0)
+        if show_mat and self.plots:
+            utils.show_gram(phi, figdir=self.figdir, gatys=self.gatys)
+        return phi
+
+    def l_bfgs(self, phi_c, phi_s, epochs, lambd, gamma, x0=None, log=print):
+        """methods.py:140-181 with scipy L-BFGS-B driving ast_loss_grad."""
+        from scipy.optimize import minimize
+        eng = self.build(self.batch_size, lambd=lambd) if lambd != self.engine.lambd else self.engine
+        self.engine = eng
+        eng.set_targets(torch.as_tensor(phi_c, dtype=torch.float32),
+                        torch.as_tensor(phi_s, dtype=torch.float32))
+        T = self.batch_size
+        x = np.zeros(T) + 1e-6 if x0 is None else np.asarray(x0, dtype=np.float64)  # methods.py:49-54
+        xd = torch.empty(1, T, device=self.device)
+        state = {'i': 0, 'i_': 0, 'since': time.time()}
+        history = []
+
+        def fg(v):
+            xd.copy_(torch.from_numpy(v.astype(np.float32)).view(1, T))
+            parts, grad = eng.loss_grad(xd)
+            reg = 0.0
+            if gamma != 0.0:
+                r, gr = stft_regularizer(xd)
+                grad = grad + gamma * gr
+                reg = float(r[0])
+            p = parts[0].cpu().numpy().astype(np.float64)
+            loss = float(p[0]) + gamma * reg
+            history.append((loss, float(p[1]), float(p[2]), reg))
+            if not state['i'] % 5:                                       # methods.py:152-155
+                log('Ep {0:}/{1:}-it {2:}({3:})-tlapse {4:.4f}s-loss{5:.4f}-{6:.4f}-{7:.4f}-{8:.4f}'.format(
+                    state['ep'] + 1, epochs, state['i'], state['i_'], time.time() - state['since'],
+                    loss, p[1], p[2], reg))
+            state['i'] += 1
+            return loss, grad[0].double().cpu().numpy()
+
+        for ep in range(epochs):
+            state['ep'], state['i'] = ep, 0
+            res = minimize(fg, x, jac=True, method='L-BFGS-B', options={'maxiter': 100})
+            x = res.x
+            state['i_'] = state['i']
+            audio = utils.inv_mu_law_numpy(x[None])[0, self.late:-self.late]
+            sp = os.path.join(self.savepath, 'ep-{}.wav'.format(ep))
+            utils.write_wav(sp, audio / np.max(audio), sr=self.sr)        # methods.py:176
+            if self.plots:
+                _, grams = eng.embeds(torch.tensor(x[None], dtype=torch.float32, device=self.device),
+                                      content=False)
+                utils.show_gram(grams[0].cpu().numpy(), ep + 1, self.figdir, gatys=self.gatys)
+            if state['i_'] < 50:                                          # methods.py:180-181
+                break
+        self.history = history
+        return x
+
+    def run(self, cont_file, source, target, epochs, lambd=0.1, gamma=0.1, audio_channel=0,
+            start=1.0):
+        """methods.py:183-216."""
+        phi_t = self.get_style_phi(target)
+        phi_s = self.get_style_phi(source, show_mat=False)
+        aud, _ = utils.load_audio(cont_file, sr=self.sr, audio_channel=audio_channel)
+        st = int(start * self.sr - self.late)
+        aud = aud[st:st + self.batch_size]
+        utils.write_wav(os.path.join(self.savepath, 'ori.wav'), aud[self.late:-self.late], self.sr)
+        style_aud, _ = utils.load_audio(target, sr=self.sr, audio_channel=audio_channel)
+        style_aud = style_aud[st:st + self.batch_size]
+        utils.write_wav(os.path.join(self.savepath, 'style.wav'), style_aud[self.late:-self.late], self.sr)
+        phi_c = self.get_embeds(aud)
+        phi = self.get_embeds(aud, is_content=False)
+        phi = phi + phi_t - phi_s
+        phi = phi / np.sqrt(np.maximum(np.sum(phi * phi, axis=(1, 2), keepdims=True), 1e-12))
+        x = self.l_bfgs(phi_c, phi, epochs=epochs, lambd=lambd, gamma=gamma)
+        return utils.inv_mu_law_numpy(x[None])[0]
+
+
+def get_dir(dir, args):
+    """methods.py:219-220 (reference-only flags excluded from the name)."""
+    kw = {k: v for k, v in vars(args).items() if k not in EXTRA_FLAGS}
+    return utils.gt_s_path(utils.crt_t_fol(dir), **kw)
+
+
+def get_fpath(fn, args):
+    return os.path.join(args.dir, fn) + '.wav'
+
+
+EXTRA_FLAGS = ('precision', 'weights', 'no_plots')
+
+
+def piece_work(args):
+    """methods.py:227-240."""
+    savepath, logdir = map(lambda d: get_dir(d, args), [args.outdir, args.logdir])
+    figdir = os.path.join(savepath, 'fig')
+    os.makedirs(figdir, exist_ok=True)
+    content, style = map(lambda name: get_fpath(name, args), [args.cont_fn, args.style_fn])
+    weights = load_weights(args.weights) if args.weights else None
+    test = GatysNet(savepath, args.ckpt_path, logdir, figdir, args.stack, args.batch_size, args.sr,
+                    args.cont_lyrs, args.channels, args.cnt_channels, args.gatys, args.style_lyrs,
+                    precision=args.precision, weights=weights, plots=not args.no_plots)
+    return test.run(content, content, style, epochs=args.epochs, lambd=args.lambd,
+                    gamma=args.gamma, start=args.start)
+
+
+def make_parser():
+    """methods.py:244-267, plus --precision / --weights / --no_plots."""
+    parser = argparse.ArgumentParser()
+    parser.add_argument('cont_fn', help='relative content file name')
+    parser.add_argument('style_fn', help='relative style file name')
+    parser.add_argument('--epochs', help='number of epochs, each epoch contains 100 iterations of optimization',
+                        nargs='?', type=int, default=100)
+    parser.add_argument('--batch_size', help='length of output signal, must be divided by 4096', nargs='?', type=int, default=16384)
+    parser.add_argument('--sr', help='sampling rate, default to 16kHz', nargs='?', type=int, default=16000)
+    parser.add_argument('--stack', help='stack of layers chosen for computing style loss. Have effects only if style_lyrs is None. There are 3 stacks, each of 10 layers. If None'
+                                        ' then all three stacks will be taken into account', nargs='?', type=int, default=None)
+    parser.add_argument('--cont_lyrs', nargs='*', type=int, default=[29])
+    parser.add_argument('--style_lyrs', nargs='*', type=int)
+    parser.add_argument('--lambd', help='style loss scalar coefficient', nargs='?', type=float, default=100.0)
+    parser.add_argument('--gamma', help='regularizer scalar coefficient', nargs='?', type=float, default=0.0)
+    parser.add_argument('--channels', help='how many channels taken into account for style loss', nargs='?', type=int, default=128)
+    parser.add_argument('--cnt_channels', help='how many channels taken into account for content loss', nargs='?', type=int, default=128)
+    parser.add_argument('--start', nargs='?', type=float, default=1.0)
+    parser.add_argument('--gatys', nargs='?', type=bool, default=False, const=True)
+    parser.add_argument('--ckpt_path', help="path to the pretrained model's checkpoint path", nargs='?', default='./nsynth/model/wavenet-ckpt/model.ckpt-200000')
+    parser.add_argument('--dir', help='path to source files, should be where to store reference style and content files', nargs='?', default='./data/src')
+    parser.add_argument('--outdir', help='path to output', nargs='?', default='./data/out')
+    parser.add_argument('--logdir', help='path to logs', nargs='?', default='./log')
+    parser.add_argument('--cmt')
+    parser.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'],
+                        help='fp32: reference numerics; bf16: bf16 storage + bf16 MFMA')
+    parser.add_argument('--weights', default=None, help='npz of TF-named encoder weights')
+    parser.add_argument('--no_plots', action='store_true', help='skip the Gram PNGs')
+    return parser
+
+
+def main(argv=None):
+    args = make_parser().parse_args(argv)
+    return piece_work(args)
+
+
+if __name__ == '__main__':
+    main(sys.argv[1:])

@@ -91,6 +91,30 @@ def reference_vectors():
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def reference_cli():
+    """The methods.py argparse surface (methods.py:244-267) as data: every add_argument call's
+    option strings and literal keywords (type= by name)."""
+    tree = ast.parse(open(os.path.join(REF, 'methods.py')).read())
+    opts = []
+    for node in ast.walk(tree):
+        if (isinstance(node, ast.Call) and isinstance(node.func, ast.Attribute)
+                and node.func.attr == 'add_argument'):
+            names = [a.value for a in node.args]
+            kw = {}
+            for k in node.keywords:
+                v = k.value
+                if isinstance(v, ast.Name):
+                    kw[k.arg] = v.id
+                elif isinstance(v, ast.Constant):
+                    kw[k.arg] = v.value
+                elif isinstance(v, ast.List):
+                    kw[k.arg] = [e.value for e in v.elts]
+            kw.pop('help', None)
+            opts.append({'names': names, 'kwargs': kw})
+    with open(os.path.join(HERE, 'reference_cli.json'), 'w') as f:
+        json.dump(opts, f, indent=1, sort_keys=True)
+
+
 def oracle_vectors():
     sys.path.insert(0, REPO)
     from oracle import astyle_oracle as O
@@ -124,5 +148,6 @@ if __name__ == '__main__':
     a = ap.parse_args()
     if not a.skip_reference:
         reference_vectors()
+        reference_cli()
     oracle_vectors()
     print('fixtures written to', HERE)

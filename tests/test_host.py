@@ -1,0 +1,84 @@
+"""CPU: the drop-in host layer (methods.py CLI surface, style-layer resolution, output naming,
+audio I/O) — no GPU."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from audio_style_transfer_amd import methods, utils
+from audio_style_transfer_amd.engine import resolve_style_ids
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+
+def test_cli_surface_matches_reference():
+    """Every option of the reference CLI (methods.py:244-267) exists with the same type,
+    default and nargs (reference_cli.json was extracted from the reference's source)."""
+    with open(os.path.join(GOLD, 'reference_cli.json')) as f:
+        ref = json.load(f)
+    parser = methods.make_parser()
+    actions = {tuple(a.option_strings) or (a.dest,): a for a in parser._actions}
+    for opt in ref:
+        key = tuple(opt['names'])
+        assert key in actions, key
+        a = actions[key]
+        kw = opt['kwargs']
+        if 'type' in kw:
+            assert a.type.__name__ == kw['type'], key
+        if 'default' in kw:
+            assert a.default == kw['default'], key
+        if 'nargs' in kw:
+            assert a.nargs == kw['nargs'], key
+        if 'const' in kw:
+            assert a.const == kw['const'], key
+
+
+def test_cli_parses_readme_example():
+    """README.md:17 example."""
+    a = methods.make_parser().parse_args(
+        'pachelbel organ --epochs 100 --cont_lyrs 25 --stack 0 --lambd 100 --gamma 0'.split())
+    assert a.cont_lyrs == [25] and a.stack == 0 and a.lambd == 100.0 and a.gamma == 0.0
+    assert a.batch_size == 16384 and a.gatys is False and a.precision == 'fp32'
+    assert methods.make_parser().parse_args(['a', 'b', '--gatys']).gatys is True
+
+
+def test_output_dir_ignores_added_flags(tmp_path):
+    a = methods.make_parser().parse_args(['pachelbel', 'organ', '--stack', '0', '--precision', 'bf16'])
+    d = methods.get_dir(str(tmp_path), a)
+    assert 'precision' not in d and os.path.isdir(d)
+    assert os.path.basename(d).startswith('ours__btch_16384_')
+
+
+def test_style_layer_resolution():
+    """methods.py:60-66."""
+    assert resolve_style_ids(None, None) == list(range(30))
+    assert resolve_style_ids(1, None) == list(range(10, 20))
+    assert resolve_style_ids(0, [3, 7]) == [3, 7]
+    with pytest.raises(AssertionError):
+        resolve_style_ids(None, 5)
+
+
+def test_wav_roundtrip_and_channel_select(tmp_path):
+    from scipy.io import wavfile
+    sr = 16000
+    t = np.arange(sr) / sr
+    st = np.stack([np.sin(2 * np.pi * 440 * t), 0.5 * np.sin(2 * np.pi * 220 * t)], axis=1)
+    p = str(tmp_path / 'a.wav')
+    wavfile.write(p, sr, (st * 32767).astype(np.int16))
+    a0, r = utils.load_audio(p, sr, audio_channel=0)
+    a1, _ = utils.load_audio(p, sr, audio_channel=1)
+    assert r == sr and a0.dtype == np.float32 and a0.shape == (sr,)
+    assert abs(np.max(np.abs(a0)) - 1.0) < 1e-3 and abs(np.max(np.abs(a1)) - 0.5) < 1e-3
+    a8, r8 = utils.load_audio(p, 8000, audio_channel=0)
+    assert r8 == 8000 and a8.shape == (sr // 2,)
+    q = str(tmp_path / 'b.wav')
+    utils.write_wav(q, a0, sr)
+    b, _ = utils.load_audio(q, sr)
+    assert np.array_equal(b, a0)
+
+
+def test_late_and_start_offsets():
+    """methods.py:39 and 195: st = int(start*sr - late)."""
+    late = (16384 - (16384 // 4096) * 4000) // 2
+    assert late == 192 and int(1.0 * 16000 - late) == 15808
