@@ -80,6 +80,8 @@ struct ast_ctx {
     void* chain[2] = {};
     float* bott = nullptr; float* gbott = nullptr;
     float* gpart = nullptr; float* smat = nullptr; float* spart = nullptr; float* cpart = nullptr;
+    u16* smatb = nullptr;                   // bf16 S~ (Gatys, precision 1)
+    size_t gpart_elems = 0, smat_elems = 0; // per context (mode-dependent)
     int ncpart = 0;
     std::vector<void*> allocs;
     const float* phi_c = nullptr; int phi_c_shared = 0;
@@ -104,7 +106,6 @@ int plan(const ast_cfg* c, ast_ctx* x) {
         return fail(AST_E_ARG, "need 1..32 content and style taps");
     if (c->cnt_channels < 1 || c->nb_channels < 1)
         return fail(AST_E_ARG, "cnt_channels / nb_channels must be >= 1");
-    if (c->gatys) return fail(AST_E_ARG, "gatys Gram is not built in this version");
     if (c->precision != 0 && c->precision != 1) return fail(AST_E_ARG, "precision must be 0 (fp32) or 1 (bf16)");
     int top = 0;
     x->need_bott = false;
@@ -141,10 +142,21 @@ int plan(const ast_cfg* c, ast_ctx* x) {
     // every dilation used must divide T (masked.py:134)
     const int maxd = x->nblk >= 10 ? 512 : (1 << (x->nblk - 1));
     if (c->T % maxd) return fail(AST_E_ARG, "T must be a multiple of the largest dilation");
-    // Gram time chunks: ~4096 workgroups, chunk a multiple of GT
-    int target = std::max(1, 4096 / (8 * c->batch));
     int nch = 1;
-    while (nch * 2 <= target && (c->T / GT) % (nch * 2) == 0) nch *= 2;
+    if (c->gatys) {
+        // Gatys Gram time chunks: >= ~2048 workgroups over (clip, tensor, chunk), chunk a
+        // multiple of 64 rows
+        const int target = std::max(1, 2048 / (c->batch * x->nu));
+        while (nch * 2 <= target && (c->T / 64) % (nch * 2) == 0) nch *= 2;
+        x->gpart_elems = (size_t)c->batch * nch * x->nu * C * C;
+        x->smat_elems = (size_t)c->batch * x->nu * C * C;
+    } else {
+        // channel-wise Gram time chunks: ~4096 workgroups, chunk a multiple of GT
+        const int target = std::max(1, 4096 / (8 * c->batch));
+        while (nch * 2 <= target && (c->T / GT) % (nch * 2) == 0) nch *= 2;
+        x->gpart_elems = (size_t)c->batch * nch * C * 1024;
+        x->smat_elems = (size_t)c->batch * C * 1024;
+    }
     x->nchunk = nch;
     return 0;
 }
@@ -162,8 +174,8 @@ size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
         if (x->tensor_has_direct_content[t] || (t == 30 && x->need_bott)) ++ncg;
     n += (size_t)ncg * BTC * es;
     if (x->need_bott) n += 2 * (size_t)c->batch * c->T * 16 * 4;
-    n += (size_t)c->batch * x->nchunk * C * 1024 * 4;       // gpart
-    n += (size_t)c->batch * C * 1024 * 4;                   // smat
+    n += x->gpart_elems * 4;                                // gpart
+    n += x->smat_elems * (c->gatys && es == 2 ? 6 : 4);     // smat (+ bf16 copy)
     n += (size_t)c->batch * C * 4;                          // spart
     n += (size_t)c->batch * x->occ.size() * (c->T / CROWS) * 4;
     return n;
@@ -254,6 +266,28 @@ StyleArgs style_args(ast_ctx* x) {
     return a;
 }
 
+GatysArgs gatys_args(ast_ctx* x) {
+    GatysArgs g;
+    memset(&g, 0, sizeof(g));
+    g.act = x->act; g.actw = x->act; g.tstride = x->tstride;
+    g.nu = x->nu;
+    for (int u = 0; u < x->nu; ++u) { g.uid[u] = x->uid[u]; g.cg[u] = x->cg_buf[x->uid[u]]; }
+    g.gpart = x->gpart; g.smat = x->smat; g.smatb = x->smatb;
+    g.B = x->cfg.batch; g.T = x->cfg.T; g.nchunk = x->nchunk;
+    return g;
+}
+
+GatysStyleArgs gatys_style_args(ast_ctx* x) {
+    GatysStyleArgs a;
+    memset(&a, 0, sizeof(a));
+    a.gpart = x->gpart; a.nchunk = x->nchunk;
+    a.L = x->L; a.nu = x->nu;
+    for (int i = 0; i < x->L; ++i) a.lmap[i] = x->lmap[i];
+    a.coef = x->cfg.lambd * 1e3f * 2.0f / (float)(x->L * C * C);
+    a.B = x->cfg.batch;
+    return a;
+}
+
 }  // namespace
 
 extern "C" {
@@ -308,8 +342,9 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
         ALLOC(x->bott, (size_t)c.batch * c.T * 16 * 4);
         ALLOC(x->gbott, (size_t)c.batch * c.T * 16 * 4);
     }
-    ALLOC(x->gpart, (size_t)c.batch * x->nchunk * C * 1024 * 4);
-    ALLOC(x->smat, (size_t)c.batch * C * 1024 * 4);
+    ALLOC(x->gpart, x->gpart_elems * 4);
+    ALLOC(x->smat, x->smat_elems * 4);
+    if (c.gatys && x->bf) ALLOC(x->smatb, x->smat_elems * 2);
     ALLOC(x->spart, (size_t)c.batch * C * 4);
     x->ncpart = (int)x->occ.size() * (c.T / CROWS);
     ALLOC(x->cpart, (size_t)c.batch * x->ncpart * 4);
@@ -428,7 +463,13 @@ int ast_embeds(ast_ctx* x, const float* xd, float* emb_c, float* emb_s, void* st
             launch_content(a, s);
         }
     }
-    if (emb_s) {
+    if (emb_s && c.gatys) {
+        GatysArgs g = gatys_args(x);
+        launch_gatys_fwd(g, x->bf, s);
+        GatysStyleArgs a = gatys_style_args(x);
+        a.embs = emb_s;
+        launch_style_gatys(a, s);
+    } else if (emb_s) {
         GramArgs g = gram_args(x);
         launch_gram_fwd_any(x, g, s);
         StyleArgs a = style_args(x);
@@ -484,17 +525,30 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
         else launch_bottleneck_bwd(x->gbott, (float*)x->cg_buf[30], x->wts + WB_OFF, !first_cg[30], c.batch, c.T, s);
     }
     // style (methods.py:62-76, 118-119)
-    GramArgs g = gram_args(x);
     tmark(x, s);
-    launch_gram_fwd_any(x, g, s);
-    tmark(x, s);
-    StyleArgs sa = style_args(x);
-    sa.phi = x->phi_s;
-    sa.phi_bstride = x->phi_s_shared ? 0 : (size_t)sa.nb * x->L * x->L;
-    sa.smat = x->smat; sa.spart = x->spart;
-    launch_style_ours(sa, s);
-    tmark(x, s);
-    launch_gram_bwd_any(x, g, s);
+    if (c.gatys) {
+        GatysArgs g = gatys_args(x);
+        launch_gatys_fwd(g, x->bf, s);
+        tmark(x, s);
+        GatysStyleArgs sa = gatys_style_args(x);
+        sa.phi = x->phi_s;
+        sa.phi_bstride = x->phi_s_shared ? 0 : (size_t)x->L * C * C;
+        sa.smat = x->smat; sa.smatb = x->smatb; sa.spart = x->spart;
+        launch_style_gatys(sa, s);
+        tmark(x, s);
+        launch_gatys_bwd(g, x->bf, s);
+    } else {
+        GramArgs g = gram_args(x);
+        launch_gram_fwd_any(x, g, s);
+        tmark(x, s);
+        StyleArgs sa = style_args(x);
+        sa.phi = x->phi_s;
+        sa.phi_bstride = x->phi_s_shared ? 0 : (size_t)sa.nb * x->L * x->L;
+        sa.smat = x->smat; sa.spart = x->spart;
+        launch_style_ours(sa, s);
+        tmark(x, s);
+        launch_gram_bwd_any(x, g, s);
+    }
     tmark(x, s);
     // backward chain through the blocks
     for (int l = x->nblk - 1; l >= 0; --l) {
@@ -527,8 +581,12 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     if (x->bf) launch_startconv_bwd((const u16*)x->chain[0], grad, x->wts + W0_OFF, c.batch, c.T, s);
     else launch_startconv_bwd((const float*)x->chain[0], grad, x->wts + W0_OFF, c.batch, c.T, s);
     const int nb = std::min(c.nb_channels, C);
-    launch_finalize(parts, x->cpart, x->ncpart, 10.0f / ((float)c.T * (float)x->ncc), x->spart, C,
-                    1e3f / (float)(nb * x->L * x->L), c.lambd, c.batch, s);
+    if (c.gatys)
+        launch_finalize(parts, x->cpart, x->ncpart, 10.0f / ((float)c.T * (float)x->ncc), x->spart,
+                        x->nu, 1e3f / (float)(x->L * C * C), c.lambd, c.batch, s);
+    else
+        launch_finalize(parts, x->cpart, x->ncpart, 10.0f / ((float)c.T * (float)x->ncc), x->spart,
+                        C, 1e3f / (float)(nb * x->L * x->L), c.lambd, c.batch, s);
     tmark(x, s);
     HIPCHK(hipGetLastError());
     if (x->timing && x->ev_used <= (int)x->ev.size()) x->timed_calls++;

@@ -116,6 +116,27 @@ struct StyleArgs {
     int B;
 };
 
+// Gatys Gram (methods.py:70-72 with --gatys): G_u = E_u^T E_u [C][C] per unique tensor.
+struct GatysArgs {
+    const void* act; void* actw; size_t tstride;
+    int nu; int uid[32];
+    const void* cg[32];                     // content grad per unique tensor (bwd) or null
+    float* gpart;                           // [B][nchunk][nu][C][C]
+    const float* smat;                      // [B][nu][C][C]  S~ = sum_l dG_l + dG_l^T (fp32)
+    const u16* smatb;                       // same, bf16 (precision 1)
+    int B, T, nchunk;
+};
+
+struct GatysStyleArgs {
+    const float* gpart; int nchunk;
+    int L; int lmap[32]; int nu;
+    const float* phi; size_t phi_bstride;   // [B|1][L][C][C]
+    float coef;                             // lambd * 1e3 * 2 / (L * C * C)
+    float* smat; u16* smatb; float* spart;  // [B][nu][C][C] (x2), [B][nu]
+    float* embs;                            // optional normalised Gram out [B][L][C][C]
+    int B;
+};
+
 struct ContentArgs {
     const void* e; int W;                   // tensor [B][T][W] (float, or bf16 when e_bf16)
     int e_bf16, cg_bf16;
@@ -151,6 +172,10 @@ void launch_gram_bwd_bf16(const GramArgs& a, hipStream_t s);
 void launch_gram_fwd(const GramArgs& a, hipStream_t s);
 void launch_gram_bwd(const GramArgs& a, hipStream_t s);
 void launch_style_ours(const StyleArgs& a, hipStream_t s);
+void launch_gatys_fwd(const GatysArgs& a, bool bf16, hipStream_t s);
+void launch_gatys_bwd(const GatysArgs& a, bool bf16, hipStream_t s);
+void launch_style_gatys(const GatysStyleArgs& a, hipStream_t s);
+constexpr int GY_ROWS = 512;    // Gatys bwd: time rows per workgroup
 void launch_content(const ContentArgs& a, hipStream_t s);
 constexpr int CROWS = 64;   // rows per content workgroup
 void launch_finalize(float* parts, const float* cpart, int ncpart, float cscale,

@@ -1,0 +1,389 @@
+// Gatys Gram (--gatys, methods.py:70-72): per style slot l, G_l = E_l^T E_l over time, a
+// [C][C] = 128 x 128 channel Gram; l2-normalised per matrix (methods.py:74), no nb_channels
+// truncation (methods.py:75 applies to "ours" only).  Gradient: S~_u = sum_{l -> u} dG_l +
+// dG_l^T folded onto unique tensors, D_u = E_u S~_u (+ content grad), in place over E_u.
+//
+//   fwd  one workgroup per (clip, tensor, time chunk); 4 waves each own a 2x2 block of 32x32
+//        output tiles; time tiles stream HBM -> LDS with global_load_lds (no VGPR staging),
+//        double-buffered.  bf16: the LDS image is row-major [t][c] (256-B rows, 16-B chunks
+//        XOR-swizzled by (row & 3) << 2 through the per-lane SOURCE address) and the MFMA
+//        operands, which need 8 consecutive time steps of one channel, come out of
+//        ds_read_b64_tr_b16 (hardware transpose, 2 reads per 32x32x16 fragment).
+//   bwd  D^T = S~ E^T: A = S~ (LDS, symmetric), B = E rows straight from HBM (each lane reads
+//        contiguous 16-B pieces of its own time row; the K order is permuted identically on
+//        both operands so a lane's 8 k-steps walk one 128-B half row), C lands as 4
+//        consecutive channels per lane -> 8-B (bf16) / 16-B (fp32) stores of the same rows.
+#include "common.h"
+
+namespace ast {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+#define LDS_AS __attribute__((address_space(3)))
+
+constexpr int GYB = 64;   // bf16 fwd: time rows per stage (16 KB)
+constexpr int GYF = 32;   // fp32 fwd: time rows per stage (16 KB)
+constexpr int SBS = 136;  // bwd bf16 S~ LDS row stride (272 B: ds_read_b128 conflict-free)
+constexpr int SFS = 129;  // bwd fp32 S~ LDS row stride (odd: ds_read_b32 conflict-free)
+
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds(g, (LDS_AS void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void gatys_decode(const GatysArgs& a, int& b, int& u, int& ch) {
+    int bid = blockIdx.x;
+    ch = bid % a.nchunk; bid /= a.nchunk;
+    u = bid % a.nu;
+    b = bid / a.nu;
+}
+
+__device__ __forceinline__ void store_gpart(const GatysArgs& a, int b, int u, int ch,
+                                            const f32x16 (&acc)[2][2], int w, int lane) {
+    float* G = a.gpart + (((size_t)b * a.nchunk + ch) * a.nu + u) * (C * C);
+    const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int I = 2 * (w >> 1) + ii, J = 2 * (w & 1) + jj;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int row = 32 * I + (q & 3) + 8 * (q >> 2) + 4 * h;
+                G[row * C + 32 * J + col] = acc[ii][jj][q];
+            }
+        }
+}
+
+__global__ void __launch_bounds__(256) k_gatys_fwd_bf16(GatysArgs a) {
+    __shared__ __attribute__((aligned(1024))) u16 Ls[2][GYB * C];
+    int b, u, ch;
+    gatys_decode(a, b, u, ch);
+    const int tlen = a.T / a.nchunk;
+    const int nt = tlen / GYB;
+    const u16* E = (const u16*)a.act + (size_t)a.uid[u] * a.tstride +
+                   ((size_t)b * a.T + (size_t)ch * tlen) * C;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // staging: wave w, instruction j fills rows (4w + j) * 4 + lane / 16, physical chunk lane % 16
+    int srcoff[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int r = (4 * w + j) * 4 + (lane >> 4), p = lane & 15;
+        srcoff[j] = r * C + ((p ^ ((r & 3) << 2)) * 8);
+    }
+    auto load = [&](int k, int buf) {
+        const u16* src = E + (size_t)k * GYB * C;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) glds16(src + srcoff[j], &Ls[buf][(4 * w + j) * 512]);
+    };
+    // transposed-read addresses (elements): row 8*kg + q (+16 s + 4 r), swizzled column
+    const int kg = lane >> 5, g16 = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
+    int aoff[2], boff[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int I = 2 * (w >> 1) + t, J = 2 * (w & 1) + t;
+        aoff[t] = (8 * kg + q) * C + (((4 * I + 2 * g16 + (p >> 1)) ^ (q << 2)) * 8) + (p & 1) * 4;
+        boff[t] = (8 * kg + q) * C + (((4 * J + 2 * g16 + (p >> 1)) ^ (q << 2)) * 8) + (p & 1) * 4;
+    }
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+            for (int e = 0; e < 16; ++e) acc[ii][jj][e] = 0.f;
+    load(0, 0);
+    for (int k = 0; k < nt; ++k) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (k + 1 < nt) load(k + 1, (k + 1) & 1);
+        const u16* Lb = Ls[k & 1];
+#pragma unroll
+        for (int s = 0; s < GYB / 16; ++s) {
+            s16x8 fa[2], fb[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (LDS_AS s16x4*)(Lb + aoff[t] + (16 * s) * C));
+                const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (LDS_AS s16x4*)(Lb + aoff[t] + (16 * s + 4) * C));
+                const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (LDS_AS s16x4*)(Lb + boff[t] + (16 * s) * C));
+                const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (LDS_AS s16x4*)(Lb + boff[t] + (16 * s + 4) * C));
+                fa[t] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+                fb[t] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj)
+                    acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        __builtin_bit_cast(bf16x8, fa[ii]), __builtin_bit_cast(bf16x8, fb[jj]),
+                        acc[ii][jj], 0, 0, 0);
+        }
+    }
+    store_gpart(a, b, u, ch, acc, w, lane);
+}
+
+__global__ void __launch_bounds__(256) k_gatys_fwd_f32(GatysArgs a) {
+    __shared__ __attribute__((aligned(1024))) float Ls[2][GYF * C];
+    int b, u, ch;
+    gatys_decode(a, b, u, ch);
+    const int tlen = a.T / a.nchunk;
+    const int nt = tlen / GYF;
+    const float* E = (const float*)a.act + (size_t)a.uid[u] * a.tstride +
+                     ((size_t)b * a.T + (size_t)ch * tlen) * C;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    auto load = [&](int k, int buf) {
+        // wave w, instruction j fills rows (4w + j) * 2 + lane / 32 (1 KiB, lane-linear)
+        const float* src = E + (size_t)k * GYF * C + lane * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) glds16(src + (4 * w + j) * 256, &Ls[buf][(4 * w + j) * 256]);
+    };
+    const int r = lane & 31, kk = lane >> 5;
+    const int I0 = 2 * (w >> 1), J0 = 2 * (w & 1);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+            for (int e = 0; e < 16; ++e) acc[ii][jj][e] = 0.f;
+    load(0, 0);
+    for (int k = 0; k < nt; ++k) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (k + 1 < nt) load(k + 1, (k + 1) & 1);
+        const float* Lb = Ls[k & 1] + kk * C + r;
+#pragma unroll 4
+        for (int s = 0; s < GYF / 2; ++s) {
+            const float* row = Lb + 2 * s * C;
+            const float a0 = row[32 * I0], a1 = row[32 * I0 + 32];
+            const float b0 = row[32 * J0], b1 = row[32 * J0 + 32];
+            acc[0][0] = mfma_f32(a0, b0, acc[0][0]);
+            acc[0][1] = mfma_f32(a0, b1, acc[0][1]);
+            acc[1][0] = mfma_f32(a1, b0, acc[1][0]);
+            acc[1][1] = mfma_f32(a1, b1, acc[1][1]);
+        }
+    }
+    store_gpart(a, b, u, ch, acc, w, lane);
+}
+
+// ---------------------------------------------------------------------------------------
+// backward: D_u[t][:] = E_u[t][:] S~_u (+ cg_u[t][:]), in place over E_u
+
+__global__ void __launch_bounds__(256) k_gatys_bwd_bf16(GatysArgs a) {
+    __shared__ __attribute__((aligned(16))) u16 Sb[C * SBS];
+    const int tilesPer = a.T / GY_ROWS;
+    int bid = blockIdx.x;
+    const int tile = bid % tilesPer; bid /= tilesPer;
+    const int u = bid % a.nu, b = bid / a.nu;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u16* S = a.smatb + ((size_t)b * a.nu + u) * (C * C);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int i = tid + 256 * k, row = i >> 4, c16 = i & 15;
+        *reinterpret_cast<uint4*>(&Sb[row * SBS + c16 * 8]) =
+            *reinterpret_cast<const uint4*>(S + row * C + c16 * 8);
+    }
+    u16* E = (u16*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;
+    const u16* CG = (const u16*)a.cg[u];
+    if (CG) CG += (size_t)b * a.T * C;
+    const int j = lane & 31, kg = lane >> 5;
+    const int rows_w = GY_ROWS / 4;
+    const int t0 = tile * GY_ROWS + w * rows_w;
+    auto loadB = [&](int t, uint4 (&bb)[8]) {
+        const uint4* src = reinterpret_cast<const uint4*>(E + (size_t)(t + j) * C + kg * 64);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) bb[s] = src[s];
+    };
+    uint4 bcur[8], bnxt[8];
+    loadB(t0, bcur);
+    __syncthreads();
+    const u16* Ab = Sb + j * SBS + kg * 64;
+    for (int n = 0; n < rows_w / 32; ++n) {
+        const int t = t0 + 32 * n;
+        if (n + 1 < rows_w / 32) loadB(t + 32, bnxt);
+        f32x16 acc[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                acc[m] = mfma_bf16(*reinterpret_cast<const uint4*>(Ab + 32 * m * SBS + 8 * s),
+                                   bcur[s], acc[m]);
+        // lane holds time t + j, channels 32m + 8g + 4kg + 0..3 in acc[m][4g..4g+3]
+        u16* out = E + (size_t)(t + j) * C + 4 * kg;
+        const u16* cgr = CG ? CG + (size_t)(t + j) * C + 4 * kg : nullptr;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int c = 32 * m + 8 * g;
+                float v0 = acc[m][4 * g], v1 = acc[m][4 * g + 1], v2 = acc[m][4 * g + 2],
+                      v3 = acc[m][4 * g + 3];
+                if (cgr) {
+                    const uint2 cv = *reinterpret_cast<const uint2*>(cgr + c);
+                    v0 += bflo(cv.x); v1 += bfhi(cv.x); v2 += bflo(cv.y); v3 += bfhi(cv.y);
+                }
+                *reinterpret_cast<uint2*>(out + c) = make_uint2(pack2(v0, v1), pack2(v2, v3));
+            }
+        if (n + 1 < rows_w / 32) {
+#pragma unroll
+            for (int s = 0; s < 8; ++s) bcur[s] = bnxt[s];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_gatys_bwd_f32(GatysArgs a) {
+    __shared__ float Sf[C * SFS];
+    const int tilesPer = a.T / GY_ROWS;
+    int bid = blockIdx.x;
+    const int tile = bid % tilesPer; bid /= tilesPer;
+    const int u = bid % a.nu, b = bid / a.nu;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float* S = a.smat + ((size_t)b * a.nu + u) * (C * C);
+    for (int i = tid; i < C * C; i += 256) Sf[(i >> 7) * SFS + (i & 127)] = S[i];
+    __syncthreads();
+    float* E = (float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;
+    const float* CG = (const float*)a.cg[u];
+    if (CG) CG += (size_t)b * a.T * C;
+    const int j = lane & 31, kg = lane >> 5;
+    const int rows_w = GY_ROWS / 4;
+    const int t0 = tile * GY_ROWS + w * rows_w;
+    const float* Ab = Sf + j * SFS + kg * 64;
+    for (int n = 0; n < rows_w / 32; ++n) {
+        const int t = t0 + 32 * n;
+        float bf[64];
+        const float4* src = reinterpret_cast<const float4*>(E + (size_t)(t + j) * C + kg * 64);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const float4 v = src[s];
+            bf[4 * s] = v.x; bf[4 * s + 1] = v.y; bf[4 * s + 2] = v.z; bf[4 * s + 3] = v.w;
+        }
+        f32x16 acc[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 64; ++s)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) acc[m] = mfma_f32(Ab[32 * m * SFS + s], bf[s], acc[m]);
+        float* out = E + (size_t)(t + j) * C + 4 * kg;
+        const float* cgr = CG ? CG + (size_t)(t + j) * C + 4 * kg : nullptr;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int c = 32 * m + 8 * g;
+                float4 v = make_float4(acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2],
+                                       acc[m][4 * g + 3]);
+                if (cgr) {
+                    const float4 cv = *reinterpret_cast<const float4*>(cgr + c);
+                    v.x += cv.x; v.y += cv.y; v.z += cv.z; v.w += cv.w;
+                }
+                *reinterpret_cast<float4*>(out + c) = v;
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// style loss: one workgroup per (clip, unique tensor); l2-normalise (methods.py:74), loss vs
+// phi (methods.py:118-119), d/dG through the normalisation, S~ = sum dG + dG^T.
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void __launch_bounds__(256) k_style_gatys(GatysStyleArgs a) {
+    __shared__ float Tt[C * SFS];
+    __shared__ float red[4];
+    const int u = blockIdx.x % a.nu, b = blockIdx.x / a.nu;
+    const int tid = threadIdx.x;
+    constexpr int NE = C * C / 256;   // 64 elements per thread: e = tid + 256 k
+    float g[NE];
+#pragma unroll
+    for (int k = 0; k < NE; ++k) g[k] = 0.f;
+    for (int ch = 0; ch < a.nchunk; ++ch) {
+        const float* src = a.gpart + (((size_t)b * a.nchunk + ch) * a.nu + u) * (C * C);
+#pragma unroll
+        for (int k = 0; k < NE; ++k) g[k] += src[tid + 256 * k];
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) ss = fmaf(g[k], g[k], ss);
+    ss = block_sum(ss, red);
+    const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+    const float big = ss >= 1e-12f ? 1.f : 0.f;
+    float sacc[NE];
+#pragma unroll
+    for (int k = 0; k < NE; ++k) sacc[k] = 0.f;
+    float sd = 0.f;
+    for (int l = 0; l < a.L; ++l) {
+        if (a.lmap[l] != u) continue;
+        if (a.embs) {
+            float* dst = a.embs + ((size_t)b * a.L + l) * (C * C);
+#pragma unroll
+            for (int k = 0; k < NE; ++k) dst[tid + 256 * k] = g[k] * inv;
+        }
+        if (!a.phi) continue;
+        const float* phi = a.phi + (size_t)b * a.phi_bstride + (size_t)l * (C * C);
+        float dgn[NE];
+        float dot = 0.f;
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            const float gn = g[k] * inv;
+            const float diff = gn - phi[tid + 256 * k];
+            sd = fmaf(diff, diff, sd);
+            dgn[k] = a.coef * diff;
+            dot = fmaf(gn, dgn[k], dot);
+        }
+        dot = block_sum(dot, red);
+#pragma unroll
+        for (int k = 0; k < NE; ++k) sacc[k] += dgn[k] * inv - big * (g[k] * inv) * dot * inv;
+    }
+    if (!a.phi) return;
+    sd = block_sum(sd, red);
+    if (tid == 0 && a.spart) a.spart[(size_t)b * a.nu + u] = sd;
+    // S~ = S + S^T through an LDS image
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int e = tid + 256 * k;
+        Tt[(e >> 7) * SFS + (e & 127)] = sacc[k];
+    }
+    __syncthreads();
+    float* sm = a.smat ? a.smat + ((size_t)b * a.nu + u) * (C * C) : nullptr;
+    u16* smb = a.smatb ? a.smatb + ((size_t)b * a.nu + u) * (C * C) : nullptr;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int e = tid + 256 * k, r = e >> 7, c = e & 127;
+        const float v = Tt[r * SFS + c] + Tt[c * SFS + r];
+        if (sm) sm[e] = v;
+        if (smb) smb[e] = f2bf(v);
+    }
+}
+
+void launch_gatys_fwd(const GatysArgs& a, bool bf16, hipStream_t s) {
+    const dim3 g(a.B * a.nu * a.nchunk);
+    if (bf16) hipLaunchKernelGGL(k_gatys_fwd_bf16, g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_gatys_fwd_f32, g, dim3(256), 0, s, a);
+}
+void launch_gatys_bwd(const GatysArgs& a, bool bf16, hipStream_t s) {
+    const dim3 g(a.B * a.nu * (a.T / GY_ROWS));
+    if (bf16) hipLaunchKernelGGL(k_gatys_bwd_bf16, g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_gatys_bwd_f32, g, dim3(256), 0, s, a);
+}
+void launch_style_gatys(const GatysStyleArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_style_gatys, dim3(a.B * a.nu), dim3(256), 0, s, a);
+}
+
+}  // namespace ast

@@ -23,6 +23,8 @@ CASES = {
                cnt_channels=128),
     'trunc': dict(cont_ids=[25, 31], style_ids=[3, 7], gatys=False, nb_channels=64,
                   cnt_channels=16),
+    'gatys': dict(cont_ids=[29], style_ids=list(range(30)), gatys=True, nb_channels=128,
+                  cnt_channels=128),
 }
 
 
@@ -90,7 +92,7 @@ def test_extracts_match_oracle(T, weights, dev):
         assert e <= 1e-5, (i, e)
 
 
-@pytest.mark.parametrize('tag', ['ours', 'trunc'])
+@pytest.mark.parametrize('tag', ['ours', 'trunc', 'gatys'])
 def test_embeds_match_oracle(tag, weights, dev):
     T = 2048
     kw = CASES[tag]
@@ -103,6 +105,34 @@ def test_embeds_match_oracle(tag, weights, dev):
     emb_c, emb_s = eng.embeds(torch.tensor(xmu[None], dtype=torch.float32, device=dev))
     assert rel(emb_c.cpu().numpy()[0], ref_c) <= 1e-5
     assert rel(emb_s.cpu().numpy()[0], ref_s) <= 1e-5
+
+
+@pytest.mark.parametrize('precision,tol', [('fp32', 2e-3), ('bf16', None)])
+def test_gatys_duplicate_taps(precision, tol, weights, dev):
+    """--gatys with repeated / aliased style taps (extracts 29 and 30 are one tensor,
+    model.py:119) and a tensor that is both a content and a style tap: the S~ fold and the
+    in-place D + content-grad add."""
+    T = 1024
+    kw = dict(cont_ids=[4, 29], style_ids=[29, 30, 2, 4], gatys=True, nb_channels=128,
+              cnt_channels=64)
+    xc = O.mu_law_numpy(synthetic_clips(1, T, 1000)[0])
+    xs = O.mu_law_numpy(synthetic_clips(1, T, 5000)[0])
+    phi_c, phi_s = O.targets_from_audio(weights, xc, [xs], [xc], **kw)
+    x = O.mu_law_numpy(synthetic_clips(1, T, 42)[0]) + np.random.default_rng(5).normal(0, 4, T)
+    ref_parts, ref_g = O.loss_and_grad(x, weights, phi_c=phi_c, phi_s=phi_s, lambd=100.0, **kw)
+    eng = _engine(2, T, kw, weights, precision=precision)
+    eng.set_targets(torch.tensor(phi_c, dtype=torch.float32), torch.tensor(phi_s, dtype=torch.float32))
+    parts, grad = eng.loss_grad(torch.tensor(np.stack([x, x]), dtype=torch.float32, device=dev))
+    parts, grad = parts.cpu().numpy(), grad.cpu().numpy()
+    assert np.array_equal(grad[0], grad[1])
+    ptol = 1e-4 if tol else 1e-2
+    for k in range(3):
+        assert abs(parts[0][k] - ref_parts[k]) <= ptol * abs(ref_parts[k]) + 1e-7, (k, parts[0], ref_parts)
+    if tol:
+        assert rel(grad[0], ref_g) <= tol, rel(grad[0], ref_g)
+    else:
+        cos = float(np.dot(grad[0], ref_g) / np.linalg.norm(grad[0]) / np.linalg.norm(ref_g))
+        assert cos >= 0.98 and rel(grad[0], ref_g) <= 0.25, (cos, rel(grad[0], ref_g))
 
 
 def test_batch_and_shard_invariance(weights, dev):
@@ -234,3 +264,14 @@ def test_bf16_batch_invariance(weights, dev):
     for b in range(3):
         p1, g1 = eng1.loss_grad(x3[b:b + 1].contiguous())
         assert torch.equal(p1[0], p3[b]) and torch.equal(g1[0], g3[b]), b
+
+
+def test_bf16_gatys_embeds(weights, dev):
+    T = 2048
+    kw = CASES['gatys']
+    xmu = O.mu_law_numpy(synthetic_clips(1, T, 1000)[0])
+    ext, _ = O.encoder_forward(xmu, weights, 30)
+    ref_s = O.style_embeds(ext, kw['style_ids'], True)
+    eng = _engine(1, T, kw, weights, precision='bf16')
+    _, emb_s = eng.embeds(torch.tensor(xmu[None], dtype=torch.float32, device=dev), content=False)
+    assert rel(emb_s.cpu().numpy()[0], ref_s) <= 2e-2
