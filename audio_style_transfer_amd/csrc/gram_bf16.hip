@@ -63,13 +63,18 @@ __global__ void __launch_bounds__(256) k_gram_fwd_bf16(GramArgs a) {
 #pragma unroll
     for (int cc = 0; cc < 4; ++cc)
         for (int i = 0; i < 16; ++i) acc[cc][i] = 0.f;
-    for (int t0 = tbeg; t0 < tbeg + tlen; t0 += 32) {
-        uint4 in[8], out[8];
+    uint4 in[8];
+    auto load = [&](int t0) {
 #pragma unroll
         for (int k = 0; k < 8; ++k)
             in[k] = src ? *reinterpret_cast<const uint4*>(src + (size_t)(t0 + stb * 8 + k) * C)
                         : make_uint4(0, 0, 0, 0);
+    };
+    load(tbeg);
+    for (int t0 = tbeg; t0 < tbeg + tlen; t0 += 32) {
+        uint4 out[8];
         transpose8(in, out);
+        if (t0 + 32 < tbeg + tlen) load(t0 + 32);   // next stage in flight during this one
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 8; ++j)

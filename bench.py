@@ -38,6 +38,8 @@ def parse():
     ap.add_argument('--clips', type=int, default=256, help='clips per GPU (batch)')
     ap.add_argument('--T', type=int, default=16384)
     ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
+    ap.add_argument('--gatys', action='store_true',
+                    help='configs[4]: Gatys [L,128,128] Gram instead of the channel-wise one')
     ap.add_argument('--lr', type=float, default=2.0)
     ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0,
                     help='CPU oracle sample budget (0 disables)')
@@ -136,7 +138,7 @@ def main():
     B, T = args.clips, args.T
     cont_ids, style_ids = [29], list(range(30))
     eng = StyleEngine(B, T, cont_ids, style_ids, precision=args.precision, device=dev,
-                      lambd=100.0)
+                      lambd=100.0, gatys=args.gatys)
     x = make_problem(eng, B, T, rank, dev)
     m = torch.zeros_like(x)
     v = torch.zeros_like(x)
@@ -201,8 +203,10 @@ def main():
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
         'dtype': args.precision,
         'data': 'synthetic (seeded sinusoid+noise clips, seeded uniform_unit_scaling weights)',
-        'config': {'workload': 'configs[2]: %dx%d clips per GPU, 30-block encoder, ours-Gram '
-                               'L=30, cont_lyrs [29], lambd 100, gamma 0, Adam step' % (B, T),
+        'config': {'workload': ('configs[4]: %dx%d clips per GPU, 30-block encoder, Gatys Gram '
+                                if args.gatys else
+                                'configs[2]: %dx%d clips per GPU, 30-block encoder, ours-Gram ')
+                               % (B, T) + 'L=30, cont_lyrs [29], lambd 100, gamma 0, Adam step',
                    'global_batch_clips': ws * B, 'T': T, 'parallelism': 'clip-sharded x%d' % ws,
                    'precision': args.precision},
         'clip_iters_per_s': value * 256.0,
