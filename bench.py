@@ -37,7 +37,11 @@ def parse():
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--clips', type=int, default=256, help='clips per GPU (batch)')
     ap.add_argument('--T', type=int, default=16384)
-    ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
+    ap.add_argument('--precision', default='bf16', choices=['fp32', 'bf16'],
+                    help='bf16: bf16 storage + bf16 MFMA, fp32 accumulation (throughput mode); '
+                         'fp32: fp32 storage + fp32 MFMA (parity mode)')
+    ap.add_argument('--fp32-steps', type=int, default=2,
+                    help='also time the fp32 parity mode for this many steps (N=1 only; 0 = off)')
     ap.add_argument('--gatys', action='store_true',
                     help='configs[4]: Gatys [L,128,128] Gram instead of the channel-wise one')
     ap.add_argument('--lr', type=float, default=2.0)
@@ -130,14 +134,12 @@ def cpu_baseline(T, budget_s):
             'clip_evals_per_s': clip_evals_per_s}
 
 
-def main():
-    args = parse()
-    ws, rank, local = dist_setup()
-    dev = torch.device('cuda', local)
+def run(args, precision, steps, warmup, ws, rank, dev):
+    """Build the engine, warm up, time `steps` steps (barrier + sync on both sides, max over
+    ranks).  Returns (seconds, engine timing dict, first loss, last loss)."""
     from audio_style_transfer_amd.engine import StyleEngine
     B, T = args.clips, args.T
-    cont_ids, style_ids = [29], list(range(30))
-    eng = StyleEngine(B, T, cont_ids, style_ids, precision=args.precision, device=dev,
+    eng = StyleEngine(B, T, [29], list(range(30)), precision=precision, device=dev,
                       lambd=100.0, gatys=args.gatys)
     x = make_problem(eng, B, T, rank, dev)
     m = torch.zeros_like(x)
@@ -152,7 +154,7 @@ def main():
         eng.loss_grad(x, grad, parts)
         eng.adam_step(x, m, v, grad, step, lr=args.lr)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         one_step()
     torch.cuda.synchronize()
     first_loss = parts[:, 0].mean().item()
@@ -160,7 +162,7 @@ def main():
     barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         one_step()
     torch.cuda.synchronize()
     barrier(ws)
@@ -171,7 +173,27 @@ def main():
     last_loss = parts[:, 0].mean().item()
     if not np.isfinite(last_loss):
         raise SystemExit('non-finite loss')
+    eng.close()
+    del x, m, v, grad, parts
+    torch.cuda.empty_cache()
+    return el, tm, first_loss, last_loss
 
+
+def main():
+    args = parse()
+    ws, rank, local = dist_setup()
+    dev = torch.device('cuda', local)
+    B, T = args.clips, args.T
+    L = 30
+    el, tm, first_loss, last_loss = run(args, args.precision, args.steps, args.warmup, ws,
+                                        rank, dev)
+    fp32_side = None
+    if args.fp32_steps > 0 and args.precision != 'fp32' and ws == 1:
+        el32, _, _, _ = run(args, 'fp32', args.fp32_steps, 1, ws, rank, dev)
+        fp32_side = {'value': B * args.fp32_steps / 256.0 / el32, 'unit': 'iters/s',
+                     'steps': args.fp32_steps,
+                     'note': 'same workload with fp32 storage + fp32 MFMA (parity mode: grad '
+                             'within 2e-3 rel-L2 of the fp64 oracle)'}
     if rank != 0:
         barrier(ws)
         return
@@ -181,21 +203,40 @@ def main():
     fwd_ms = tm['block_fwd_ms'] / (calls * nblk)
     bwd_ms = tm['block_bwd_ms'] / (calls * nblk)
     launch_ms = (fwd_ms + bwd_ms) / 2
-    flops_per_launch = 131072.0 * T * B          # 2*(384+128)*128 flop per row, fwd or bwd
-    achieved_tflops = flops_per_launch / (launch_ms * 1e-3) / 1e12
-    peak = FP32_MFMA_PEAK_TFLOPS if args.precision == 'fp32' else BF16_MFMA_PEAK_TFLOPS
+    esz = 4.0 if args.precision == 'fp32' else 2.0
+    A = B * T * 128 * esz                          # one activation tensor, all clips
+    flops_per_launch = 131072.0 * T * B            # 2*(384+128)*128 flop per row, fwd or bwd
+    bytes_per_launch = 2.5 * A                     # fwd 2A (read e_l, write e_l+1), bwd 3A
     traffic = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get('precision') == args.precision and tj.get('clips') == B and tj.get('T') == T:
+        if (tj.get('precision') == args.precision and tj.get('clips') == B and tj.get('T') == T):
             traffic = tj['block_bytes_per_launch']
     except Exception:
         traffic = None
+    if args.precision == 'fp32':
+        # fp32: 96 flop/B on the dilated conv, above the fp32 ridge -> MFMA-bound
+        achieved = flops_per_launch / (launch_ms * 1e-3) / 1e12
+        roof = {'bound': 'mfma', 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS,
+                'unit': 'TFLOP/s', 'frac': achieved / FP32_MFMA_PEAK_TFLOPS}
+    else:
+        # bf16 storage: 192 flop/B fwd (below the 312 flop/B bf16 ridge) -> HBM-bound
+        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        roof = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': achieved / HBM_PEAK_GBS}
+    roof.update({'traffic': traffic,
+                 'kernel': 'k_block_fwd*/k_block_bwd* (fused dilated conv + 1x1 + epilogues), '
+                           'mean of one fwd and one bwd launch',
+                 'algorithmic_bytes_per_launch': bytes_per_launch,
+                 'flops_per_launch': flops_per_launch,
+                 'mfma_frac': flops_per_launch / (launch_ms * 1e-3) / 1e12 /
+                              (FP32_MFMA_PEAK_TFLOPS if args.precision == 'fp32'
+                               else BF16_MFMA_PEAK_TFLOPS),
+                 'avg_launch_ms': launch_ms, 'fwd_launch_ms': fwd_ms, 'bwd_launch_ms': bwd_ms})
     gram_fwd_ms = tm['gram_fwd_ms'] / calls
     gram_bwd_ms = tm['gram_bwd_ms'] / calls
-    L = len(style_ids)
-    gram_bytes = L * B * T * 128 * (4.0 if args.precision == 'fp32' else 2.0)
+    gram_bytes = L * A
     out = {
         'metric': 'style-transfer iters/sec, 256x16384-sample batch, 30-layer WaveNet encoder',
         'value': value, 'unit': 'iters/s', 'n_gpus': ws, 'steps': args.steps,
@@ -210,11 +251,7 @@ def main():
                    'global_batch_clips': ws * B, 'T': T, 'parallelism': 'clip-sharded x%d' % ws,
                    'precision': args.precision},
         'clip_iters_per_s': value * 256.0,
-        'roofline': {'kernel': 'k_block_fwd/k_block_bwd (fused dilated conv + 1x1 + epilogues)',
-                     'bound': 'mfma', 'achieved': achieved_tflops, 'peak': peak,
-                     'unit': 'TFLOP/s', 'frac': achieved_tflops / peak, 'traffic': traffic,
-                     'flops_per_launch': flops_per_launch, 'avg_launch_ms': launch_ms,
-                     'fwd_launch_ms': fwd_ms, 'bwd_launch_ms': bwd_ms},
+        'roofline': roof,
         'kernels_ms_per_step': {'block_fwd': tm['block_fwd_ms'] / calls,
                                 'block_bwd': tm['block_bwd_ms'] / calls,
                                 'gram_fwd': gram_fwd_ms, 'gram_bwd': gram_bwd_ms,
@@ -224,6 +261,8 @@ def main():
                           'peak': HBM_PEAK_GBS},
         'loss_first_last': [first_loss, last_loss],
     }
+    if fp32_side:
+        out['fp32_mode'] = fp32_side
     if ws == 1 and args.cpu_baseline_seconds > 0:
         out['cpu_baseline'] = cpu_baseline(T, args.cpu_baseline_seconds)
     print(json.dumps(out), flush=True)

@@ -52,7 +52,10 @@ def main(tag, precision, clips, T):
     summary = {'tag': tag, 'precision': precision, 'clips': clips, 'T': T, 'kernels': stats}
     with open(os.path.join(dst, tag + '_summary.json'), 'w') as f:
         json.dump(summary, f, indent=1)
-    fw, bw = stats.get('k_block_fwd', {}), stats.get('k_block_bwd', {})
+    def pick(prefix):   # fp32 'k_block_fwd' or bf16 'k_block_fwd_bf16' (either layout variant)
+        ks = [k for k in stats if k.startswith(prefix) and 'hbm_bytes_per_launch' in stats[k]]
+        return max((stats[k] for k in ks), key=lambda v: v['calls'], default={})
+    fw, bw = pick('k_block_fwd'), pick('k_block_bwd')
     if 'hbm_bytes_per_launch' in fw and 'hbm_bytes_per_launch' in bw:
         tj = {'precision': precision, 'clips': clips, 'T': T, 'source': tag,
               'block_bytes_per_launch': (fw['hbm_bytes_per_launch'] + bw['hbm_bytes_per_launch']) / 2,
