@@ -71,32 +71,20 @@ def barrier(ws):
         dist.barrier()
 
 
-def max_over_ranks(v, ws):
-    if ws == 1:
-        return v
-    import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device='cuda')
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def make_problem(eng, B, T, rank, dev):
-    """Synthetic per-clip targets (SURVEY §8d): content clip c_b, style clip s_b;
-    phi_c = emb_c(c_b); phi_s = l2norm(G^(c_b) + G^(s_b) - G^(c_b)) (methods.py:207-212 with
-    one clip per file)."""
-    from audio_style_transfer_amd.weights import synthetic_clips
-    from audio_style_transfer_amd.utils import mu_law_numpy
-    cont = torch.tensor(mu_law_numpy(synthetic_clips(B, T, 1000 + rank * B)), dtype=torch.float32,
-                        device=dev)
-    sty = torch.tensor(mu_law_numpy(synthetic_clips(B, T, 5000 + rank * B)), dtype=torch.float32,
-                       device=dev)
+def make_problem(eng, clips, T, dev):
+    """Synthetic per-clip targets for the global clip indices `clips`: content
+    clip c_g, style clip s_g; phi_c = emb_c(c_g); phi_s = l2norm(G^(c_g) + G^(s_g) - G^(c_g))
+    (methods.py:207-212 with one clip per file); x0 = c_g + 4 N(0,1) (seeded per clip)."""
+    from audio_style_transfer_amd.shard import shard_inputs
+    cont, sty, x0 = shard_inputs(clips, T)
+    cont = torch.tensor(cont, device=dev)
+    sty = torch.tensor(sty, device=dev)
     phi_c, g_c = eng.embeds(cont)
     _, g_s = eng.embeds(sty, content=False)
     phi = g_c + g_s - g_c
     phi = phi / phi.pow(2).sum(dim=(-2, -1), keepdim=True).clamp_min(1e-12).sqrt()
     eng.set_targets(phi_c, phi)
-    x = (cont + torch.randn_like(cont) * 4.0).contiguous()
-    return x
+    return torch.tensor(x0, device=dev)
 
 
 def cpu_baseline(T, budget_s):
@@ -141,7 +129,8 @@ def run(args, precision, steps, warmup, ws, rank, dev):
     B, T = args.clips, args.T
     eng = StyleEngine(B, T, [29], list(range(30)), precision=precision, device=dev,
                       lambd=100.0, gatys=args.gatys)
-    x = make_problem(eng, B, T, rank, dev)
+    from audio_style_transfer_amd.shard import clip_range
+    x = make_problem(eng, clip_range(ws * B, ws, rank), T, dev)
     m = torch.zeros_like(x)
     v = torch.zeros_like(x)
     grad = torch.empty_like(x)
@@ -167,7 +156,8 @@ def run(args, precision, steps, warmup, ws, rank, dev):
     torch.cuda.synchronize()
     barrier(ws)
     el = time.perf_counter() - t0
-    el = max_over_ranks(el, ws)
+    from audio_style_transfer_amd.shard import max_over_ranks
+    el = max_over_ranks(el, ws, device=dev)
     tm = eng.timing_read()
     eng.timing(False)
     last_loss = parts[:, 0].mean().item()
