@@ -49,7 +49,7 @@ def stft_regularizer(x: torch.Tensor):
     a = sgn / 255.0 * (256.0 ** abs_tf(o) - 1)
     a = torch.where(x == 0, x, a)
     S = torch.stft(a, n_fft=1024, hop_length=512, win_length=1024,
-                   window=torch.hann_window(1024, periodic=True, device=x.device),
+                   window=torch.hann_window(1024, periodic=True, dtype=x.dtype, device=x.device),
                    center=False, return_complex=True)
     reg = (abs_tf(S.real) + abs_tf(S.imag)).mean(dim=(-2, -1))
     g, = torch.autograd.grad(reg.sum(), x)
