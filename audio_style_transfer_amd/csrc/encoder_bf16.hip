@@ -110,9 +110,8 @@ __device__ __forceinline__ bool is_center(int L, const Layout& ly) {
     return k >= 1 && k <= ly.M;
 }
 
-// e > 0 mask of one staged 256-B row, assembled by its 16 lanes (q = lane & 15); lane q=0
-// returns the 4 words (channels 0-31, 32-63, ...).
-__device__ __forceinline__ uint4 row_sign_bits(uint4 v, int q, int lane) {
+// e > 0 bits of 8 bf16 channels (bit k = channel k)
+__device__ __forceinline__ uint32_t sign_bits8(uint4 v) {
     const uint32_t d[4] = {v.x, v.y, v.z, v.w};
     uint32_t bits = 0;
 #pragma unroll
@@ -120,13 +119,7 @@ __device__ __forceinline__ uint4 row_sign_bits(uint4 v, int q, int lane) {
         bits |= ((short)(d[j] & 0xffffu) > 0 ? 1u : 0u) << (2 * j);
         bits |= ((short)(d[j] >> 16) > 0 ? 1u : 0u) << (2 * j + 1);
     }
-    uint32_t m = bits << (8 * (q & 3));
-    m |= (uint32_t)__shfl_xor((int)m, 1);
-    m |= (uint32_t)__shfl_xor((int)m, 2);
-    const uint32_t w1 = (uint32_t)__shfl((int)m, lane + 4);
-    const uint32_t w2 = (uint32_t)__shfl((int)m, lane + 8);
-    const uint32_t w3 = (uint32_t)__shfl((int)m, lane + 12);
-    return make_uint4(m, w1, w2, w3);
+    return bits;
 }
 
 __device__ __forceinline__ void load_bias16(float (&bias)[16], const float* src, int h) {
@@ -174,10 +167,16 @@ __global__ void __launch_bounds__(NTH, 1) k_block_fwd_bf16(FwdArgsB a, Layout ly
     build_tables(ROWM, ROWS, RMAP, ly, tid);
     __syncthreads();
 
-    // prefetch registers: piece j of this thread = LDS row (tid + j*NTH) >> 4, 16 B at q*8
+    // Prefetch registers: piece j of this thread = LDS row (tid + j*NTH) >> 4, 16 B at q*8.
+    // Every global load and store of the tile loop is unconditional (zero rows, rows past
+    // the layout and tiles past the end load a clamped valid address and are masked), and
+    // the loop is rotated so the prefetch of tile i+1 is committed to LDS at the END of
+    // iteration i: the compiler then counts the wait for it in straight-line code, behind
+    // this tile's stores (vmcnt(N)), instead of draining the stores with vmcnt(0).
     uint4 pf[PF_K];
+    uint32_t pfm[PF_K];
     auto prefetch = [&](int tile, int* TTn) {
-        if (tile >= ntiles) return;
+        tile = tile < ntiles ? tile : ntiles - 1;
         const int b = tile / tiles, p0 = (tile - b * tiles) * TMB;
         const int m0 = p0 % a.n, j0 = p0 / a.n;
         const u16* src = a.ein + (size_t)b * a.T * C;
@@ -185,15 +184,25 @@ __global__ void __launch_bounds__(NTH, 1) k_block_fwd_bf16(FwdArgsB a, Layout ly
         for (int j = 0; j < PF_K; ++j) {
             const int i = tid + j * NTH;
             const int L = i >> 4;
-            pf[j] = make_uint4(0, 0, 0, 0);
-            if (L < ly.nrows) {
-                const int t = tile_row_time<MASKED>(L, p0, m0, j0, ROWM, ROWS, ly, a.T, a.n, a.d);
-                if ((i & 15) == 0) TTn[L] = t;
-                if (t >= 0) pf[j] = *reinterpret_cast<const uint4*>(src + (uint32_t)(t * C + (i & 15) * 8));
-            }
+            const int t = L < ly.nrows ? tile_row_time<MASKED>(L, p0, m0, j0, ROWM, ROWS, ly, a.T, a.n, a.d) : -1;
+            if ((i & 15) == 0 && L < NRMAX) TTn[L] = t;
+            pfm[j] = t >= 0 ? 0xffffffffu : 0u;
+            pf[j] = *reinterpret_cast<const uint4*>(src + (uint32_t)((t >= 0 ? t : 0) * C + (i & 15) * 8));
+        }
+    };
+    auto commit = [&]() {
+#pragma unroll
+        for (int j = 0; j < PF_K; ++j) {
+            const int i = tid + j * NTH;
+            const int L = i >> 4, q = i & 15;
+            if (L >= ly.nrows) break;
+            const uint4 v = make_uint4(pf[j].x & pfm[j], pf[j].y & pfm[j], pf[j].z & pfm[j], pf[j].w & pfm[j]);
+            *reinterpret_cast<uint4*>(&X[L * XSB + q * 8]) = v;
+            *reinterpret_cast<uint4*>(&R[L * XSB + q * 8]) = relu8(v);
         }
     };
     prefetch(blockIdx.x, TTb[0]);
+    commit();
     int it = 0;
     STAMP_DECL
 
@@ -203,24 +212,11 @@ __global__ void __launch_bounds__(NTH, 1) k_block_fwd_bf16(FwdArgsB a, Layout ly
         const size_t cbase = (size_t)b * a.T * C;
         const size_t mbase = (size_t)b * a.T * 4;
         int* TT = TTb[it & 1];
-        uint32_t* meb = a.me + mbase;
+        uint8_t* meb = reinterpret_cast<uint8_t*>(a.me + mbase);
         STAMP(0)
-        __syncthreads();                                   // (A) previous tile consumed
-        STAMP(1)
-        // commit the prefetched rows (no global stores here: the prefetch that follows
-        // must not queue behind them)
-#pragma unroll
-        for (int j = 0; j < PF_K; ++j) {
-            const int i = tid + j * NTH;
-            const int L = i >> 4, q = i & 15;
-            if (L >= ly.nrows) break;
-            *reinterpret_cast<uint4*>(&X[L * XSB + q * 8]) = pf[j];
-            *reinterpret_cast<uint4*>(&R[L * XSB + q * 8]) = relu8(pf[j]);
-        }
-        STAMP(2)
         prefetch(tile + gridDim.x, TTb[(it + 1) & 1]);     // in flight during this tile
         STAMP(3)
-        __syncthreads();                                   // (B)
+        __syncthreads();                                   // (B) X / R / TT of this tile ready
         STAMP(4)
 
         int Lc[NJ];
@@ -298,9 +294,7 @@ __global__ void __launch_bounds__(NTH, 1) k_block_fwd_bf16(FwdArgsB a, Layout ly
         STAMP(6)
         __syncthreads();                                   // (C)
         STAMP(7)
-        if (tid < TMB)
-            *reinterpret_cast<uint4*>(a.mu + mbase + (uint32_t)(TT[RMAP[tid]] * 4)) =
-                *reinterpret_cast<const uint4*>(&MB[tid * 4]);
+        a.mu[mbase + (uint32_t)(TT[RMAP[tid >> 2]] * 4 + (tid & 3))] = MB[tid];   // 512 x 4 B
         // GEMM 2: y^T[co2][c] = sum_co Wr[co][co2] v[c][co]   (model.py:109-114)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
@@ -347,7 +341,8 @@ __global__ void __launch_bounds__(NTH, 1) k_block_fwd_bf16(FwdArgsB a, Layout ly
         STAMP(9)
         __syncthreads();                                   // (D)
         STAMP(10)
-        // write e_{l+1} rows; the e_l > 0 mask (== relu(e_l) != 0, from R) leaves with them
+        // write e_{l+1} rows; the e_l > 0 mask (== relu(e_l) != 0, from R) leaves with them,
+        // one byte (channels 8q..8q+7) per lane
         u16* dst = a.eout + cbase;
 #pragma unroll
         for (int j = 0; j < TMB * 16 / NTH; ++j) {
@@ -356,10 +351,13 @@ __global__ void __launch_bounds__(NTH, 1) k_block_fwd_bf16(FwdArgsB a, Layout ly
             const int t = TT[L];
             *reinterpret_cast<uint4*>(dst + (uint32_t)(t * C + q * 8)) =
                 *reinterpret_cast<const uint4*>(&X[L * XSB + q * 8]);
-            const uint4 mw = row_sign_bits(*reinterpret_cast<const uint4*>(&R[L * XSB + q * 8]), q, lane);
-            if (q == 0) *reinterpret_cast<uint4*>(meb + (uint32_t)(t * 4)) = mw;
+            meb[(uint32_t)(t * 16 + q)] = (uint8_t)sign_bits8(*reinterpret_cast<const uint4*>(&R[L * XSB + q * 8]));
         }
         STAMP(11)
+        __syncthreads();                                   // (A) this tile's X / R consumed
+        STAMP(1)
+        commit();                                          // next tile's rows
+        STAMP(2)
     }
     STAMP_FLUSH(a.stamps)
 }
