@@ -3,6 +3,7 @@
 // launch sequence of one loss+grad evaluation (methods.py:113-137 evaluated as
 // ScipyOptimizerInterface does, methods.py:167).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 #include <stdio.h>
 #include <string>
@@ -81,6 +82,7 @@ struct ast_ctx {
     float* bott = nullptr; float* gbott = nullptr;
     float* gpart = nullptr; float* smat = nullptr; float* spart = nullptr; float* cpart = nullptr;
     u16* smatb = nullptr;                   // bf16 S~ (Gatys, precision 1)
+    void* zero = nullptr;                   // 256 zero bytes
     size_t gpart_elems = 0, smat_elems = 0; // per context (mode-dependent)
     int ncpart = 0;
     std::vector<void*> allocs;
@@ -177,6 +179,7 @@ size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     n += x->gpart_elems * 4;                                // gpart
     n += x->smat_elems * (c->gatys && es == 2 ? 6 : 4);     // smat (+ bf16 copy)
     n += (size_t)c->batch * C * 4;                          // spart
+    n += 256;                                               // zero line
     n += (size_t)c->batch * x->occ.size() * (c->T / CROWS) * 4;
     return n;
 }
@@ -198,6 +201,17 @@ float* blkw(ast_ctx* x, int l) { return x->wts + BLK_OFF + (size_t)l * BLK_SZ; }
 u16* blkwb(ast_ctx* x, int l) { return x->wtsb + (size_t)l * BLKB_SZ; }
 void* tens(ast_ctx* x, int t) { return (char*)x->act + (size_t)t * x->tstride * x->esz; }
 
+// bf16 block-forward kernel: 0 = DMA-staged two-workgroups-per-CU (default), 1 = persistent
+// one-workgroup-per-CU (ASTYLE_FWD=persistent; kept for A/B measurement)
+int fwd_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("ASTYLE_FWD");
+        v = (e && !strcmp(e, "persistent")) ? 1 : 0;
+    }
+    return v;
+}
+
 int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
     const ast_cfg& c = x->cfg;
     if (x->bf) launch_startconv_fwd((const float*)xd, (u16*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s);
@@ -216,7 +230,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
             a.wdT = wb + WDTB; a.bd = w + BD; a.wrT = wb + WRTB; a.br = w + BR;
             a.mu = mu; a.me = me;
             a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
-            launch_block_fwd_bf16(a, s);
+            if (fwd_variant() == 1) launch_block_fwd_bf16(a, s); else launch_block_fwd_dma(a, s);
         } else {
             FwdArgs a;
             a.ein = (const float*)tens(x, l); a.eout = (float*)tens(x, l + 1);
@@ -249,7 +263,7 @@ GramArgs gram_args(ast_ctx* x) {
     g.act = x->act; g.actw = x->act; g.tstride = x->tstride;
     g.nu = x->nu;
     for (int u = 0; u < x->nu; ++u) { g.uid[u] = x->uid[u]; g.cg[u] = x->cg_buf[x->uid[u]]; }
-    g.gpart = x->gpart; g.smat = x->smat;
+    g.gpart = x->gpart; g.smat = x->smat; g.zero16 = x->zero;
     g.B = x->cfg.batch; g.T = x->cfg.T; g.nchunk = x->nchunk;
     return g;
 }
@@ -345,6 +359,8 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     ALLOC(x->gpart, x->gpart_elems * 4);
     ALLOC(x->smat, x->smat_elems * 4);
     if (c.gatys && x->bf) ALLOC(x->smatb, x->smat_elems * 2);
+    ALLOC(x->zero, 256);
+    (void)hipMemset(x->zero, 0, 256);
     ALLOC(x->spart, (size_t)c.batch * C * 4);
     x->ncpart = (int)x->occ.size() * (c.T / CROWS);
     ALLOC(x->cpart, (size_t)c.batch * x->ncpart * 4);
