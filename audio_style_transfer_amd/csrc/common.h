@@ -5,7 +5,9 @@
 //                           (model.py:116); channels-last so a time row is one 512-B line
 //                           group (fp32).  Tapped tensors are overwritten in place by their
 //                           direct loss gradient D during the Gram backward.
-//   mu/me [NB][B][T][4]     u>0 / e_l>0 relu masks, one bit per channel (16 B per row)
+//   mu/me [NB][B][T][4]     u>0 / e_l>0 relu masks, one bit per channel (16 B per row);
+//                           fp32 kernels index them by time, bf16 kernels by the layer's
+//                           time_to_batch position (a tile's masks are one contiguous run)
 //   chain [2][B][T][C]      fp32 backward ping-pong (d loss / d e_l)
 // Dilated rows are visited in time_to_batch order (masked.py:57-86): tile position p maps to
 // time t = (p % n) * d + p / n with n = T / d, so a tile's tap neighbours are p-1 / p+1 and

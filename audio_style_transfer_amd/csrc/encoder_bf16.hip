@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(NTH, 1) k_block_fwd_bf16(FwdArgsB a, Layout ly
         STAMP(6)
         __syncthreads();                                   // (C)
         STAMP(7)
-        a.mu[mbase + (uint32_t)(TT[RMAP[tid >> 2]] * 4 + (tid & 3))] = MB[tid];   // 512 x 4 B
+        a.mu[mbase + (uint32_t)((p0 + (tid >> 2)) * 4 + (tid & 3))] = MB[tid];   // 512 x 4 B, by position
         // GEMM 2: y^T[co2][c] = sum_co Wr[co][co2] v[c][co]   (model.py:109-114)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
@@ -351,7 +351,7 @@ __global__ void __launch_bounds__(NTH, 1) k_block_fwd_bf16(FwdArgsB a, Layout ly
             const int t = TT[L];
             *reinterpret_cast<uint4*>(dst + (uint32_t)(t * C + q * 8)) =
                 *reinterpret_cast<const uint4*>(&X[L * XSB + q * 8]);
-            meb[(uint32_t)(t * 16 + q)] = (uint8_t)sign_bits8(*reinterpret_cast<const uint4*>(&R[L * XSB + q * 8]));
+            meb[(uint32_t)((p0 + (i >> 4)) * 16 + q)] = (uint8_t)sign_bits8(*reinterpret_cast<const uint4*>(&R[L * XSB + q * 8]));
         }
         STAMP(11)
         __syncthreads();                                   // (A) this tile's X / R consumed
@@ -422,10 +422,11 @@ __global__ void __launch_bounds__(NTH, 1) k_block_bwd_bf16(BwdArgsB a, Layout ly
         pme = make_uint4(0, 0, 0, 0);
         if (tid < ly.nrows) {
             const int t = tile_row_time<MASKED>(tid, p0, m0, j0, ROWM, ROWS, ly, a.T, a.n, a.d);
-            if (t >= 0) {
+            if (t >= 0) {   // masks are stored by position (time_to_batch order) of this layer
+                const int pos = MASKED ? p0 - 1 + tid : p0 + ROWS[tid] * ly.M + ROWM[tid];
                 const size_t mbase = (size_t)b * a.T * 4;
-                pmu = *reinterpret_cast<const uint4*>(a.mu + mbase + (uint32_t)(t * 4));
-                pme = *reinterpret_cast<const uint4*>(a.me + mbase + (uint32_t)(t * 4));
+                pmu = *reinterpret_cast<const uint4*>(a.mu + mbase + (uint32_t)(pos * 4));
+                pme = *reinterpret_cast<const uint4*>(a.me + mbase + (uint32_t)(pos * 4));
             }
         }
     };

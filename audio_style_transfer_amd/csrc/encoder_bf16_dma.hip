@@ -231,10 +231,10 @@ __global__ void __launch_bounds__(NT2, 2) k_block_fwd_dma(FwdArgsB a, Layout2 ly
             const int i = tid + NT2 * k, cc = i >> 4, q = i & 15;
             const int L = RMAP[cc];
             const uint4 v = *reinterpret_cast<const uint4*>(X + xoff(L, q));
-            meb[(uint32_t)(TT[L] * 16 + q)] = (uint8_t)sign_byte(v);
+            meb[(uint32_t)((p0 + cc) * 16 + q)] = (uint8_t)sign_byte(v);
         }
         lds_barrier();                                      // (C) V, MB complete
-        a.mu[mbase + (uint32_t)(TT[RMAP[tid >> 2]] * 4 + (tid & 3))] = MB[tid];
+        a.mu[mbase + (uint32_t)((p0 + (tid >> 2)) * 4 + (tid & 3))] = MB[tid];
         // GEMM 2: y^T[co2][c] = sum_co Wr[co][co2] v[c][co]   (model.py:109-114)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
