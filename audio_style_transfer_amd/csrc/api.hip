@@ -201,18 +201,6 @@ float* blkw(ast_ctx* x, int l) { return x->wts + BLK_OFF + (size_t)l * BLK_SZ; }
 u16* blkwb(ast_ctx* x, int l) { return x->wtsb + (size_t)l * BLKB_SZ; }
 void* tens(ast_ctx* x, int t) { return (char*)x->act + (size_t)t * x->tstride * x->esz; }
 
-// bf16 block-forward kernel (A/B switch ASTYLE_FWD): 0 = cross-tile pipelined persistent
-// (default), 1 = DMA-staged two-workgroups-per-CU ("dma"), 2 = single-phase persistent
-// ("persistent"), 3 = two-group ping-pong ("pp")
-int fwd_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("ASTYLE_FWD");
-        v = !e ? 0 : !strcmp(e, "dma") ? 1 : !strcmp(e, "persistent") ? 2 : !strcmp(e, "pp") ? 3 : 0;
-    }
-    return v;
-}
-
 int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
     const ast_cfg& c = x->cfg;
     if (x->bf) launch_startconv_fwd((const float*)xd, (u16*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s);
@@ -231,12 +219,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
             a.wdT = wb + WDTB; a.bd = w + BD; a.wrT = wb + WRTB; a.br = w + BR;
             a.mu = mu; a.me = me;
             a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
-            switch (fwd_variant()) {
-                case 1: launch_block_fwd_dma(a, s); break;
-                case 2: launch_block_fwd_bf16(a, s); break;
-                case 3: launch_block_fwd_pp(a, s); break;
-                default: launch_block_fwd_pipe(a, s);
-            }
+            launch_block_fwd_bf16(a, s);
         } else {
             FwdArgs a;
             a.ein = (const float*)tens(x, l); a.eout = (float*)tens(x, l + 1);

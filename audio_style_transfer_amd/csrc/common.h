@@ -162,9 +162,6 @@ void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T,
 void launch_block_fwd(const FwdArgs& a, hipStream_t s);
 void launch_block_bwd(const BwdArgs& a, hipStream_t s);
 void launch_block_fwd_bf16(const FwdArgsB& a, hipStream_t s);
-void launch_block_fwd_dma(const FwdArgsB& a, hipStream_t s);
-void launch_block_fwd_pp(const FwdArgsB& a, hipStream_t s);
-void launch_block_fwd_pipe(const FwdArgsB& a, hipStream_t s);
 void launch_block_bwd_bf16(const BwdArgsB& a, hipStream_t s);
 template <typename S>
 void launch_bottleneck_fwd(const S* e, float* y, const float* wb, const float* bb,

@@ -362,224 +362,6 @@ __global__ void __launch_bounds__(NTH, 1) k_block_fwd_bf16(FwdArgsB a, Layout ly
     STAMP_FLUSH(a.stamps)
 }
 
-// Cross-tile software-pipelined variant of the forward: X is double-buffered (no relu copy:
-// relu is applied to the GEMM1 fragments after the read), the output rows of tile i-1 leave
-// from LDS interleaved with tile i's GEMM1 MFMAs, the e_l > 0 bits come from the staged rows
-// in epilogue 1, and a tile needs two barriers instead of four.
-template <bool MASKED>
-__global__ void __launch_bounds__(NTH, 1) k_block_fwd_pipe(FwdArgsB a, Layout ly) {
-    __shared__ __attribute__((aligned(16))) u16 X[2][NRMAX * XSB];  // e_l rows, then e_{l+1} in place
-    __shared__ __attribute__((aligned(16))) u16 V[TMB * XSB];       // relu(u) by column
-    __shared__ __attribute__((aligned(16))) uint32_t MB[TMB * 4];
-    __shared__ __attribute__((aligned(16))) u16 WR[C * XSB];        // Wr^T [co2][co]
-    __shared__ int TTb[3][NRMAX];                                   // row times, tile % 3
-    __shared__ int ROWM[NRMAX], ROWS[NRMAX], RMAP[TMB];
-    __shared__ __attribute__((aligned(16))) float BIAS[2 * C];
-    const int tiles = a.T / TMB;
-    const int ntiles = a.B * tiles;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r = lane & 31, h = lane >> 5;
-    const int cb = (w & 3) * 32;
-    const int nh = w >> 2;
-
-    uint4 wd[3][8];
-#pragma unroll
-    for (int tp = 0; tp < 3; ++tp)
-#pragma unroll
-        for (int kb = 0; kb < 8; ++kb)
-            wd[tp][kb] = *reinterpret_cast<const uint4*>(a.wdT + (size_t)tp * C * C + (size_t)(cb + r) * C + 8 * h + kb * 16);
-    for (int i = tid; i < C * 16; i += NTH)
-        *reinterpret_cast<uint4*>(&WR[(i >> 4) * XSB + (i & 15) * 8]) =
-            *reinterpret_cast<const uint4*>(a.wrT + (size_t)(i >> 4) * C + (i & 15) * 8);
-    if (tid < C) { BIAS[tid] = a.bd[tid]; BIAS[C + tid] = a.br[tid]; }
-    build_tables(ROWM, ROWS, RMAP, ly, tid);
-    __syncthreads();
-
-    uint4 pf[PF_K];
-    uint32_t pfm[PF_K];
-    auto prefetch = [&](int tile, int* TTn) {
-        tile = tile < ntiles ? tile : ntiles - 1;
-        const int b = tile / tiles, p0 = (tile - b * tiles) * TMB;
-        const int m0 = p0 % a.n, j0 = p0 / a.n;
-        const u16* src = a.ein + (size_t)b * a.T * C;
-#pragma unroll
-        for (int j = 0; j < PF_K; ++j) {
-            const int i = tid + j * NTH;
-            const int L = i >> 4;
-            const int t = L < ly.nrows ? tile_row_time<MASKED>(L, p0, m0, j0, ROWM, ROWS, ly, a.T, a.n, a.d) : -1;
-            if ((i & 15) == 0 && L < NRMAX) TTn[L] = t;
-            pfm[j] = t >= 0 ? 0xffffffffu : 0u;
-            pf[j] = *reinterpret_cast<const uint4*>(src + (uint32_t)((t >= 0 ? t : 0) * C + (i & 15) * 8));
-        }
-    };
-    auto commit = [&](u16* Xn) {
-#pragma unroll
-        for (int j = 0; j < PF_K; ++j) {
-            const int i = tid + j * NTH;
-            const int L = i >> 4, q = i & 15;
-            if (L >= ly.nrows) break;
-            *reinterpret_cast<uint4*>(&Xn[L * XSB + q * 8]) =
-                make_uint4(pf[j].x & pfm[j], pf[j].y & pfm[j], pf[j].z & pfm[j], pf[j].w & pfm[j]);
-        }
-    };
-    // output piece k (of TMB*16/NTH = 4) of the previous tile: LDS row -> HBM
-    auto out_piece = [&](int k, const u16* Xp, const int* TTp, u16* dstp) {
-        const int i = tid + k * NTH;
-        const int L = RMAP[i >> 4], q = i & 15;
-        *reinterpret_cast<uint4*>(dstp + (uint32_t)(TTp[L] * C + q * 8)) =
-            *reinterpret_cast<const uint4*>(&Xp[L * XSB + q * 8]);
-    };
-
-    prefetch(blockIdx.x, TTb[0]);
-    commit(X[0]);
-    prefetch(blockIdx.x + gridDim.x, TTb[1]);
-    __syncthreads();
-    int it = 0;
-    u16* dprev = nullptr;                 // output base of the previous tile (null: none)
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
-        const int b = tile / tiles;
-        const int p0 = (tile - b * tiles) * TMB;
-        const int cur = it & 1;
-        const u16* Xc = X[cur];
-        const u16* Xp = X[cur ^ 1];
-        const int* TTp = TTb[(it + 2) % 3];   // previous tile's row times
-        int Lc[NJ];
-        bool ok0[NJ], ok2[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int c = (NJ * nh + j) * 32 + r;
-            Lc[j] = RMAP[c];
-            ok0[j] = ok2[j] = true;
-            if (MASKED) {
-                const int m = (p0 + c) % a.n;
-                ok0[j] = m > 0;
-                ok2[j] = m < a.n - 1;
-            }
-        }
-        // GEMM 1 (relu on the fragments), with the previous tile's 4 output pieces in between
-        f32x16 acc[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-            for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
-        {
-            uint4 bcur[NJ], bnxt[NJ];
-            const u16* rb[NJ];
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                rb[j] = &Xc[(Lc[j] - 1) * XSB + 8 * h];
-                bcur[j] = relu8(*reinterpret_cast<const uint4*>(rb[j]));
-            }
-#pragma unroll
-            for (int st = 0; st < 24; ++st) {
-                const int tp = st >> 3, kb = st & 7;
-                if (dprev && (st % 6) == 1) out_piece(st / 6, Xp, TTp, dprev);
-                if (st + 1 < 24) {
-                    const int tn = (st + 1) >> 3, kn = (st + 1) & 7;
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j)
-                        bnxt[j] = relu8(*reinterpret_cast<const uint4*>(rb[j] + tn * XSB + kn * 16));
-                }
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    uint4 bv = bcur[j];
-                    if (MASKED) {
-                        const bool ok = tp == 0 ? ok0[j] : (tp == 2 ? ok2[j] : true);
-                        if (!ok) bv = make_uint4(0, 0, 0, 0);
-                    }
-                    acc[j] = mfma_bf16(wd[tp][kb], bv, acc[j]);
-                }
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) bcur[j] = bnxt[j];
-            }
-        }
-        {   // epilogue 1: + b_d, relu -> V; u > 0 bits -> MB; e_l > 0 bytes from the rows
-            float bias[16];
-            load_bias16(bias, BIAS + cb, h);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int c = (NJ * nh + j) * 32 + r;
-                uint32_t part = 0;
-                float v[16];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const float u = acc[j][i] + bias[i];
-                    part |= (u > 0.f ? 1u : 0u) << acc_row(i, h);
-                    v[i] = fmaxf(u, 0.f);
-                }
-                const uint32_t word = part | (uint32_t)__shfl_xor((int)part, 32);
-                if (h == 0) MB[c * 4 + (w & 3)] = word;
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    *reinterpret_cast<uint2*>(&V[c * XSB + cb + 8 * g + 4 * h]) =
-                        make_uint2(pack2(v[4 * g], v[4 * g + 1]), pack2(v[4 * g + 2], v[4 * g + 3]));
-            }
-            uint8_t* meb = reinterpret_cast<uint8_t*>(a.me + (size_t)b * a.T * 4);
-#pragma unroll
-            for (int k = 0; k < TMB * 16 / NTH; ++k) {
-                const int i = tid + k * NTH, cc = i >> 4, q = i & 15;
-                const uint4 v = *reinterpret_cast<const uint4*>(&Xc[RMAP[cc] * XSB + q * 8]);
-                meb[(uint32_t)((p0 + cc) * 16 + q)] = (uint8_t)sign_bits8(v);
-            }
-        }
-        __syncthreads();                                   // (C) V, MB complete
-        a.mu[(size_t)b * a.T * 4 + (uint32_t)((p0 + (tid >> 2)) * 4 + (tid & 3))] = MB[tid];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-            for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
-        {   // GEMM 2
-            uint4 acur, anxt, bcur[NJ], bnxt[NJ];
-            acur = *reinterpret_cast<const uint4*>(&WR[(cb + r) * XSB + 8 * h]);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-                bcur[j] = *reinterpret_cast<const uint4*>(&V[((NJ * nh + j) * 32 + r) * XSB + 8 * h]);
-#pragma unroll
-            for (int kb = 0; kb < 8; ++kb) {
-                if (kb + 1 < 8) {
-                    anxt = *reinterpret_cast<const uint4*>(&WR[(cb + r) * XSB + (kb + 1) * 16 + 8 * h]);
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j)
-                        bnxt[j] = *reinterpret_cast<const uint4*>(&V[((NJ * nh + j) * 32 + r) * XSB + (kb + 1) * 16 + 8 * h]);
-                }
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) acc[j] = mfma_bf16(acur, bcur[j], acc[j]);
-                acur = anxt;
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) bcur[j] = bnxt[j];
-            }
-        }
-        {   // epilogue 2: e_{l+1} = e_l + (y + b_r), this wave's channels of X in place
-            u16* Xw = X[cur];
-            float bias[16];
-            load_bias16(bias, BIAS + C + cb, h);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    uint2* px = reinterpret_cast<uint2*>(&Xw[Lc[j] * XSB + cb + 8 * g + 4 * h]);
-                    const uint2 ev = *px;
-                    const float o0 = bflo(ev.x) + (acc[j][4 * g + 0] + bias[4 * g + 0]);
-                    const float o1 = bfhi(ev.x) + (acc[j][4 * g + 1] + bias[4 * g + 1]);
-                    const float o2 = bflo(ev.y) + (acc[j][4 * g + 2] + bias[4 * g + 2]);
-                    const float o3 = bfhi(ev.y) + (acc[j][4 * g + 3] + bias[4 * g + 3]);
-                    *px = make_uint2(pack2(o0, o1), pack2(o2, o3));
-                }
-            }
-        }
-        // next tile's rows into the other buffer (its previous content left during GEMM1,
-        // before barrier C), then the prefetch of the tile after it
-        commit(X[cur ^ 1]);
-        prefetch(tile + 2 * gridDim.x, TTb[(it + 2) % 3]);
-        dprev = a.eout + (size_t)b * a.T * C;
-        __syncthreads();                                   // (D) e_{l+1} rows + next rows ready
-    }
-    if (dprev) {   // the last tile's output
-        const u16* Xp = X[(it - 1) & 1];
-        const int* TTp = TTb[(it - 1) % 3];
-#pragma unroll
-        for (int k = 0; k < TMB * 16 / NTH; ++k) out_piece(k, Xp, TTp, dprev);
-    }
-}
-
 template <bool MASKED>
 __global__ void __launch_bounds__(NTH, 1) k_block_bwd_bf16(BwdArgsB a, Layout ly) {
     __shared__ __attribute__((aligned(16))) u16 G[NRMAX * XSB];   // tot = g_{l+1} + D_{l+1}
@@ -834,13 +616,6 @@ void launch_block_fwd_bf16(const FwdArgsB& a, hipStream_t s) {
     Layout ly;
     if (pick_layout(a.n, ly)) hipLaunchKernelGGL(k_block_fwd_bf16<true>, grid, dim3(NTH), 0, s, a, ly);
     else hipLaunchKernelGGL(k_block_fwd_bf16<false>, grid, dim3(NTH), 0, s, a, ly);
-}
-void launch_block_fwd_pipe(const FwdArgsB& a, hipStream_t s) {
-    const int nt = a.B * (a.T / TMB);
-    const dim3 grid(std::min(nt, num_cus()));
-    Layout ly;
-    if (pick_layout(a.n, ly)) hipLaunchKernelGGL(k_block_fwd_pipe<true>, grid, dim3(NTH), 0, s, a, ly);
-    else hipLaunchKernelGGL(k_block_fwd_pipe<false>, grid, dim3(NTH), 0, s, a, ly);
 }
 void launch_block_bwd_bf16(const BwdArgsB& a, hipStream_t s) {
     const int nt = a.B * (a.T / TMB);
