@@ -16,7 +16,7 @@ MAX_TAPS = 32
 # Every symbol include/astyle.h declares (checked by tests/test_abi.py).
 EXPORTS = ('ast_create', 'ast_destroy', 'ast_workspace_bytes', 'ast_set_weight', 'ast_forward',
            'ast_get_extract', 'ast_embeds', 'ast_content_cols', 'ast_set_targets',
-           'ast_loss_grad', 'ast_adam_step', 'ast_timing', 'ast_timing_read',
+           'ast_loss_grad', 'ast_adam_step', 'ast_adam_step_dev', 'ast_timing', 'ast_timing_read',
            'ast_last_error')
 
 
@@ -59,6 +59,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         'ast_set_targets': (i, [vp, vp, i, vp, i]),
         'ast_loss_grad': (i, [vp, vp, vp, vp, vp]),
         'ast_adam_step': (i, [vp, vp, vp, vp, vp, i, f, f, f, f, vp]),
+        'ast_adam_step_dev': (i, [vp, vp, vp, vp, vp, vp, f, f, f, f, vp]),
         'ast_timing': (i, [vp, i]),
         'ast_timing_read': (i, [vp, fp, i]),
         'ast_last_error': (ctypes.c_char_p, []),

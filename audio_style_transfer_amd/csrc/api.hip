@@ -608,6 +608,14 @@ int ast_adam_step(ast_ctx* x, float* xd, float* m, float* v, const float* grad, 
     return 0;
 }
 
+int ast_adam_step_dev(ast_ctx* x, float* xd, float* m, float* v, const float* grad, int* step_dev,
+                      float lr, float b1, float b2, float eps, void* stream) {
+    if (!x || !xd || !m || !v || !grad || !step_dev) return fail(AST_E_ARG, "bad argument");
+    launch_adam_dev(xd, m, v, grad, (size_t)x->cfg.batch * x->cfg.T, step_dev, lr, b1, b2, eps, S(stream));
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 // Event layout per timed ast_loss_grad call (8 marks):
 //  m0 start | startconv | m1 | blocks fwd | m2 | content | m3 gram fwd m4 style m5 gram bwd m6
 //  | blocks bwd | m7 | startconv bwd + finalize | m8

@@ -186,5 +186,7 @@ void launch_finalize(float* parts, const float* cpart, int ncpart, float cscale,
                      hipStream_t s);
 void launch_adam(float* x, float* m, float* v, const float* g, size_t n, float lr, float b1,
                  float b2, float eps, float bc1, float bc2, hipStream_t s);
+void launch_adam_dev(float* x, float* m, float* v, const float* g, size_t n, int* step_dev,
+                     float lr, float b1, float b2, float eps, hipStream_t s);
 
 }  // namespace ast

@@ -315,6 +315,33 @@ __global__ void __launch_bounds__(256) k_adam(float* __restrict__ x, float* __re
     x[i] -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
 }
 
+// device-counter form: step = *step_dev + 1 (bias corrections computed per thread)
+__global__ void __launch_bounds__(256) k_adam_dev(float* __restrict__ x, float* __restrict__ m,
+                                                  float* __restrict__ v,
+                                                  const float* __restrict__ g, size_t n,
+                                                  const int* __restrict__ step_dev, float lr,
+                                                  float b1, float b2, float eps) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float st = (float)(*step_dev + 1);
+    const float bc1 = 1.f - powf(b1, st), bc2 = 1.f - powf(b2, st);
+    const float gi = g[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    x[i] -= lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+}
+
+__global__ void k_step_inc(int* step_dev) { *step_dev += 1; }
+
+void launch_adam_dev(float* x, float* m, float* v, const float* g, size_t n, int* step_dev,
+                     float lr, float b1, float b2, float eps, hipStream_t s) {
+    hipLaunchKernelGGL(k_adam_dev, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, m, v, g,
+                       n, step_dev, lr, b1, b2, eps);
+    hipLaunchKernelGGL(k_step_inc, dim3(1), dim3(1), 0, s, step_dev);
+}
+
 void launch_adam(float* x, float* m, float* v, const float* g, size_t n, float lr, float b1,
                  float b2, float eps, float bc1, float bc2, hipStream_t s) {
     hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, m, v, g,

@@ -76,10 +76,10 @@ class StyleEngine:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def _ptr(self, t: Optional[torch.Tensor]):
+    def _ptr(self, t: Optional[torch.Tensor], dtype=torch.float32):
         if t is None:
             return None
-        assert t.is_cuda and t.device == self.device and t.dtype == torch.float32, t
+        assert t.is_cuda and t.device == self.device and t.dtype == dtype, t
         assert t.is_contiguous()
         return ctypes.c_void_p(t.data_ptr())
 
@@ -168,6 +168,13 @@ class StyleEngine:
                                           self._ptr(grad), int(step), float(lr), float(beta1),
                                           float(beta2), float(eps), self._stream()))
 
+    def adam_step_dev(self, x, m, v, grad, step_dev, lr=1.0, beta1=0.9, beta2=0.999, eps=1e-8):
+        """Adam with the step counter in device memory (int32 tensor, incremented in place)."""
+        _lib.check(self.lib.ast_adam_step_dev(self.h, self._ptr(x), self._ptr(m), self._ptr(v),
+                                              self._ptr(grad), self._ptr(step_dev, torch.int32), float(lr),
+                                              float(beta1), float(beta2), float(eps),
+                                              self._stream()))
+
     def timing(self, enable: bool) -> None:
         _lib.check(self.lib.ast_timing(self.h, int(enable)))
 
@@ -177,3 +184,48 @@ class StyleEngine:
         keys = ('block_fwd_ms', 'block_bwd_ms', 'gram_fwd_ms', 'gram_bwd_ms', 'other_ms',
                 'calls', 'blocks')
         return dict(zip(keys, list(out)))
+
+
+class AdamLoop:
+    """The throughput-mode optimiser step on the device: ast_loss_grad + fused Adam over the
+    audio buffer ``x`` [B, T] (optimised in place; Adam state and the step counter on the
+    device).  With ``graph=True`` the step is captured once into a HIP graph
+    (torch.cuda.CUDAGraph on the capture stream) and every ``step()`` is one graph replay.
+    Capture runs one warm-up step eagerly and then restores x / m / v / the counter, so the
+    state sequence is the same either way."""
+
+    def __init__(self, eng: StyleEngine, x: torch.Tensor, lr: float = 1.0, beta1: float = 0.9,
+                 beta2: float = 0.999, eps: float = 1e-8, graph: bool = False):
+        self.eng = eng
+        self.x = x
+        self.m = torch.zeros_like(x)
+        self.v = torch.zeros_like(x)
+        self.grad = torch.empty_like(x)
+        self.parts = torch.empty(eng.batch, 4, device=x.device)
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=x.device)
+        self.hp = (float(lr), float(beta1), float(beta2), float(eps))
+        self.graph = None
+        if graph:
+            saved = [t.clone() for t in (self.x, self.m, self.v, self.step_dev)]
+            side = torch.cuda.Stream(device=x.device)
+            side.wait_stream(torch.cuda.current_stream(x.device))
+            with torch.cuda.stream(side):
+                self._eager()
+            torch.cuda.current_stream(x.device).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._eager()
+            for t, s in zip((self.x, self.m, self.v, self.step_dev), saved):
+                t.copy_(s)
+            self.graph = g
+
+    def _eager(self):
+        self.eng.loss_grad(self.x, self.grad, self.parts)
+        self.eng.adam_step_dev(self.x, self.m, self.v, self.grad, self.step_dev, *self.hp)
+
+    def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._eager()
+        return self.parts

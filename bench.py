@@ -4,8 +4,8 @@
 Gram over all 30 layers, content layer 29, lambda 100, gamma 0).
 
 One step = one loss+grad evaluation of every clip (encoder fwd -> Gram -> losses -> backward
-to the audio, ast_loss_grad) + the fused Adam update of the audio (ast_adam_step), inputs
-already resident in HBM.  N GPUs = N processes (torch.distributed.run), each owning its own
+to the audio, ast_loss_grad) + the fused Adam update of the audio (ast_adam_step_dev), inputs
+already resident in HBM, replayed from a captured HIP graph (--graph 1, default).  N GPUs = N processes (torch.distributed.run), each owning its own
 256 clips: weak scaling, no collective in the step; the barrier/max-over-ranks
 timing is the only cross-rank traffic.
 
@@ -45,6 +45,8 @@ def parse():
     ap.add_argument('--gatys', action='store_true',
                     help='configs[4]: Gatys [L,128,128] Gram instead of the channel-wise one')
     ap.add_argument('--lr', type=float, default=2.0)
+    ap.add_argument('--graph', type=int, default=1,
+                    help='1: replay the step from a captured HIP graph (default); 0: eager launches')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0,
                     help='CPU oracle sample budget (0 disables)')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'),
@@ -122,49 +124,43 @@ def cpu_baseline(T, budget_s):
             'clip_evals_per_s': clip_evals_per_s}
 
 
-def run(args, precision, steps, warmup, ws, rank, dev):
+def run(args, precision, steps, warmup, ws, rank, dev, graph):
     """Build the engine, warm up, time `steps` steps (barrier + sync on both sides, max over
-    ranks).  Returns (seconds, engine timing dict, first loss, last loss)."""
-    from audio_style_transfer_amd.engine import StyleEngine
+    ranks).  A step is one AdamLoop step (ast_loss_grad + device-counter Adam), replayed from
+    a captured HIP graph when `graph`.  The per-kernel-family breakdown comes from HIP events
+    of 2 extra eager steps (events are not recorded inside a graph).  Returns (seconds,
+    engine timing dict, first loss, last loss)."""
+    from audio_style_transfer_amd.engine import StyleEngine, AdamLoop
+    from audio_style_transfer_amd.shard import clip_range, max_over_ranks
     B, T = args.clips, args.T
     eng = StyleEngine(B, T, [29], list(range(30)), precision=precision, device=dev,
                       lambd=100.0, gatys=args.gatys)
-    from audio_style_transfer_amd.shard import clip_range
     x = make_problem(eng, clip_range(ws * B, ws, rank), T, dev)
-    m = torch.zeros_like(x)
-    v = torch.zeros_like(x)
-    grad = torch.empty_like(x)
-    parts = torch.empty(B, 4, device=dev)
-    step = 0
-
-    def one_step():
-        nonlocal step
-        step += 1
-        eng.loss_grad(x, grad, parts)
-        eng.adam_step(x, m, v, grad, step, lr=args.lr)
-
+    loop = AdamLoop(eng, x, lr=args.lr, graph=graph)
     for _ in range(warmup):
-        one_step()
+        loop.step()
     torch.cuda.synchronize()
-    first_loss = parts[:, 0].mean().item()
-    eng.timing(True)
+    first_loss = loop.parts[:, 0].mean().item()
     barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        one_step()
+        loop.step()
     torch.cuda.synchronize()
     barrier(ws)
     el = time.perf_counter() - t0
-    from audio_style_transfer_amd.shard import max_over_ranks
     el = max_over_ranks(el, ws, device=dev)
-    tm = eng.timing_read()
-    eng.timing(False)
-    last_loss = parts[:, 0].mean().item()
+    last_loss = loop.parts[:, 0].mean().item()
     if not np.isfinite(last_loss):
         raise SystemExit('non-finite loss')
+    eng.timing(True)
+    for _ in range(2):
+        loop._eager()
+    torch.cuda.synchronize()
+    tm = eng.timing_read()
+    eng.timing(False)
+    del loop, x
     eng.close()
-    del x, m, v, grad, parts
     torch.cuda.empty_cache()
     return el, tm, first_loss, last_loss
 
@@ -176,10 +172,10 @@ def main():
     B, T = args.clips, args.T
     L = 30
     el, tm, first_loss, last_loss = run(args, args.precision, args.steps, args.warmup, ws,
-                                        rank, dev)
+                                        rank, dev, args.graph)
     fp32_side = None
     if args.fp32_steps > 0 and args.precision != 'fp32' and ws == 1:
-        el32, _, _, _ = run(args, 'fp32', args.fp32_steps, 1, ws, rank, dev)
+        el32, _, _, _ = run(args, 'fp32', args.fp32_steps, 1, ws, rank, dev, args.graph)
         fp32_side = {'value': B * args.fp32_steps / 256.0 / el32, 'unit': 'iters/s',
                      'steps': args.fp32_steps,
                      'note': 'same workload with fp32 storage + fp32 MFMA (parity mode: grad '
@@ -239,7 +235,7 @@ def main():
                                 'configs[2]: %dx%d clips per GPU, 30-block encoder, ours-Gram ')
                                % (B, T) + 'L=30, cont_lyrs [29], lambd 100, gamma 0, Adam step',
                    'global_batch_clips': ws * B, 'T': T, 'parallelism': 'clip-sharded x%d' % ws,
-                   'precision': args.precision},
+                   'precision': args.precision, 'hip_graph': bool(args.graph)},
         'clip_iters_per_s': value * 256.0,
         'roofline': roof,
         'kernels_ms_per_step': {'block_fwd': tm['block_fwd_ms'] / calls,

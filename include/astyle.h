@@ -90,6 +90,10 @@ int ast_loss_grad(ast_ctx* ctx, const float* x_dev, float* grad_dev, float* part
 /* Fused Adam on the audio buffer: m, v, x updated in place from grad_dev. step >= 1. */
 int ast_adam_step(ast_ctx* ctx, float* x_dev, float* m_dev, float* v_dev, const float* grad_dev,
                   int step, float lr, float beta1, float beta2, float eps, void* stream);
+/* Same, with the step counter in device memory: uses *step_dev + 1 and stores it back, so a
+ * captured hipGraph of {ast_loss_grad, ast_adam_step_dev} replays as consecutive steps. */
+int ast_adam_step_dev(ast_ctx* ctx, float* x_dev, float* m_dev, float* v_dev, const float* grad_dev,
+                      int* step_dev, float lr, float beta1, float beta2, float eps, void* stream);
 
 /* Per-kernel-family device timing (HIP events on the call's stream).  enable!=0 starts
  * recording; ast_timing_read fills out[0..n) with milliseconds summed since enable for

@@ -275,3 +275,34 @@ def test_bf16_gatys_embeds(weights, dev):
     eng = _engine(1, T, kw, weights, precision='bf16')
     _, emb_s = eng.embeds(torch.tensor(xmu[None], dtype=torch.float32, device=dev), content=False)
     assert rel(emb_s.cpu().numpy()[0], ref_s) <= 2e-2
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+def test_graph_replay_matches_eager(precision, weights, dev):
+    """The hipGraph-captured step (loss_grad + device-counter Adam) replays bit-identically to
+    eager steps, and the device-counter Adam equals the host-counter one."""
+    from audio_style_transfer_amd.engine import AdamLoop
+    T = 2048
+    kw = CASES['ours']
+    phi_c, phi_s = _targets('ours', T, weights)
+    eng = _engine(2, T, kw, weights, precision=precision)
+    eng.set_targets(torch.tensor(phi_c, dtype=torch.float32), torch.tensor(phi_s, dtype=torch.float32))
+    x0 = torch.tensor(O.mu_law_numpy(synthetic_clips(2, T, 77)), dtype=torch.float32, device=dev)
+    runs = []
+    for graph in (False, True):
+        loop = AdamLoop(eng, x0.clone(), lr=0.5, graph=graph)
+        for _ in range(4):
+            loop.step()
+        torch.cuda.synchronize()
+        runs.append((loop.x.clone(), loop.parts.clone(), int(loop.step_dev.item())))
+    assert runs[0][2] == runs[1][2] == 4
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
+    # host-counter Adam, eager
+    x = x0.clone()
+    m = torch.zeros_like(x)
+    v = torch.zeros_like(x)
+    for k in range(1, 5):
+        _, g = eng.loss_grad(x)
+        eng.adam_step(x, m, v, g, k, lr=0.5)
+    torch.cuda.synchronize()
+    assert torch.allclose(x, runs[0][0], rtol=1e-5, atol=1e-3)   # device vs host powf
