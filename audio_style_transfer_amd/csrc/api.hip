@@ -602,7 +602,7 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
 int ast_adam_step(ast_ctx* x, float* xd, float* m, float* v, const float* grad, int step,
                   float lr, float b1, float b2, float eps, void* stream) {
     if (!x || !xd || !m || !v || !grad || step < 1) return fail(AST_E_ARG, "bad argument");
-    const float bc1 = 1.0f - powf(b1, (float)step), bc2 = 1.0f - powf(b2, (float)step);
+    const float bc1 = 1.0f - pow_int(b1, step), bc2 = 1.0f - pow_int(b2, step);
     launch_adam(xd, m, v, grad, (size_t)x->cfg.batch * x->cfg.T, lr, b1, b2, eps, bc1, bc2, S(stream));
     HIPCHK(hipGetLastError());
     return 0;

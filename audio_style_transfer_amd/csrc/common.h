@@ -184,6 +184,18 @@ constexpr int CROWS = 64;   // rows per content workgroup
 void launch_finalize(float* parts, const float* cpart, int ncpart, float cscale,
                      const float* spart, int nspart, float sscale, float lambd, int B,
                      hipStream_t s);
+// b^n by squaring: the same fp32 products on host and device, so the host-counter and the
+// device-counter Adam steps agree bit for bit
+__host__ __device__ inline float pow_int(float b, int n) {
+    float r = 1.f;
+    while (n > 0) {
+        if (n & 1) r *= b;
+        b *= b;
+        n >>= 1;
+    }
+    return r;
+}
+
 void launch_adam(float* x, float* m, float* v, const float* g, size_t n, float lr, float b1,
                  float b2, float eps, float bc1, float bc2, hipStream_t s);
 void launch_adam_dev(float* x, float* m, float* v, const float* g, size_t n, int* step_dev,

@@ -323,8 +323,8 @@ __global__ void __launch_bounds__(256) k_adam_dev(float* __restrict__ x, float* 
                                                   float b1, float b2, float eps) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const float st = (float)(*step_dev + 1);
-    const float bc1 = 1.f - powf(b1, st), bc2 = 1.f - powf(b2, st);
+    const int st = *step_dev + 1;
+    const float bc1 = 1.f - pow_int(b1, st), bc2 = 1.f - pow_int(b2, st);
     const float gi = g[i];
     const float mi = b1 * m[i] + (1.f - b1) * gi;
     const float vi = b2 * v[i] + (1.f - b2) * gi * gi;

@@ -305,4 +305,4 @@ def test_graph_replay_matches_eager(precision, weights, dev):
         _, g = eng.loss_grad(x)
         eng.adam_step(x, m, v, g, k, lr=0.5)
     torch.cuda.synchronize()
-    assert torch.allclose(x, runs[0][0], rtol=1e-5, atol=1e-3)   # device vs host powf
+    assert torch.equal(x, runs[0][0])   # same pow_int bias correction on host and device
