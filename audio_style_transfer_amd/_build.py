@@ -10,10 +10,13 @@ from concurrent.futures import ThreadPoolExecutor
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, 'csrc')
 LIB = os.path.join(PKG, 'libastyle.so')
-SOURCES = ['encoder.hip', 'encoder_bf16.hip', 'gram.hip', 'gram_bf16.hip', 'gram_gatys.hip', 'api.hip']
+SOURCES = ['encoder.hip', 'encoder_bf16.hip', 'block_fwd_bf16.hip', 'gram.hip', 'gram_bf16.hip', 'gram_gatys.hip', 'api.hip']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall',
          '-Wno-unused-function', '-munsafe-fp-atomics']
+# per-source extras: the column-owning block kernels keep their weights in AGPRs (asm-loaded)
+# and need the MFMA accumulators in arch VGPRs, where the epilogues read them without copies
+EXTRA = {'block_fwd_bf16.hip': ['-mllvm', '-amdgpu-mfma-vgpr-form=1']}
 
 
 def _stale() -> bool:
@@ -35,7 +38,7 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
 
     def cc(src):
         obj = os.path.join(objdir, src.replace('.hip', '.o'))
-        cmd = [HIPCC, *flags, '-c', os.path.join(CSRC, src), '-o', obj]
+        cmd = [HIPCC, *flags, *EXTRA.get(src, []), '-c', os.path.join(CSRC, src), '-o', obj]
         if verbose:
             print(' '.join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

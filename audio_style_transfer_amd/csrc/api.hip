@@ -45,7 +45,12 @@ constexpr size_t WB_OFF = BLK_OFF + NBLK_MAX * BLK_SZ;   // [128][16]
 constexpr size_t BB_OFF = WB_OFF + C * 16;
 constexpr size_t W_TOTAL = BB_OFF + 16;
 // bf16 copies (precision 1), u16 elements per block
-constexpr size_t WDB = 0, WDTB = 3 * C * C, WRB = 6 * C * C, WRTB = 7 * C * C, BLKB_SZ = 8 * C * C;
+constexpr size_t WDB = 0, WDTB = 3 * C * C, WRB = 6 * C * C, WRTB = 7 * C * C;
+// MFMA A-fragment order for block_fwd_bf16.hip: WFB [3 taps][4 q][8 kb][64 lanes][8],
+// lane (m, h) element e = W_d[tap][ci = 16 kb + 8 h + e][co = 32 q + m];
+// WRFB [4 q2][8 s][64][8], element e = W_r[co = kperm(s, h, e)][co2 = 32 q2 + m]
+constexpr size_t WFB = 8 * C * C, WRFB = 11 * C * C, BLKB_SZ = 12 * C * C;
+inline int kperm(int s, int h, int e) { return 32 * (s >> 1) + 16 * (s & 1) + (e & 3) + 8 * (e >> 2) + 4 * h; }
 
 uint16_t host_bf16(float f) {   // round to nearest even
     uint32_t u;
@@ -203,7 +208,7 @@ void* tens(ast_ctx* x, int t) { return (char*)x->act + (size_t)t * x->tstride * 
 
 int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
     const ast_cfg& c = x->cfg;
-    if (x->bf) launch_startconv_fwd((const float*)xd, (u16*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s);
+    if (x->bf) launch_startconv_fwd((const float*)xd, (u16*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s, (uint16_t*)x->me);
     else launch_startconv_fwd((const float*)xd, (float*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s);
     if (mark) tmark(x, s);
     for (int l = 0; l < x->nblk; ++l) {
@@ -212,14 +217,16 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
         uint32_t* mu = x->mu + (size_t)l * c.batch * c.T * 4;
         uint32_t* me = x->me + (size_t)l * c.batch * c.T * 4;
         if (x->bf) {
-            FwdArgsB a;
-            a.stamps = g_stamps;
+            FwdArgsC a;
             u16* wb = blkwb(x, l);
             a.ein = (const u16*)tens(x, l); a.eout = (u16*)tens(x, l + 1);
-            a.wdT = wb + WDTB; a.bd = w + BD; a.wrT = wb + WRTB; a.br = w + BR;
-            a.mu = mu; a.me = me;
+            a.wf = wb + WFB; a.wrf = wb + WRFB; a.bd = w + BD; a.br = w + BR;
+            a.mu = (uint16_t*)mu;
+            a.me_next = l + 1 < x->nblk ? (uint16_t*)(me + (size_t)c.batch * c.T * 4) : nullptr;
+            a.zero = (const u16*)x->zero;
             a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
-            launch_block_fwd_bf16(a, s);
+            a.dn_log2 = (l + 1) % 10; a.nn = c.T >> a.dn_log2;
+            launch_block_fwd_c(a, s);
         } else {
             FwdArgs a;
             a.ein = (const float*)tens(x, l); a.eout = (float*)tens(x, l + 1);
@@ -396,9 +403,19 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                         tr[(size_t)k * C * C + co * C + ci] = host[(size_t)k * C * C + ci * C + co];
             if ((rc = put(base + WD, host, 3 * C * C))) return rc;
             if ((rc = put(base + WDT, tr.data(), 3 * C * C))) return rc;
-            std::vector<uint16_t> hb(6 * C * C);
+            std::vector<uint16_t> hb(6 * C * C), hf(3 * C * C);
             for (size_t i = 0; i < 3 * C * C; ++i) { hb[i] = host_bf16(host[i]); hb[3 * C * C + i] = host_bf16(tr[i]); }
-            HIPCHK(hipMemcpy(x->wtsb + (size_t)(l - 1) * BLKB_SZ + WDB, hb.data(), 6 * C * C * 2, hipMemcpyHostToDevice));
+            for (int k = 0; k < 3; ++k)
+                for (int q = 0; q < 4; ++q)
+                    for (int kb = 0; kb < 8; ++kb)
+                        for (int ln = 0; ln < 64; ++ln)
+                            for (int e = 0; e < 8; ++e) {
+                                const int ci = 16 * kb + 8 * (ln >> 5) + e, co = 32 * q + (ln & 31);
+                                hf[((((size_t)k * 4 + q) * 8 + kb) * 64 + ln) * 8 + e] = hb[(size_t)k * C * C + ci * C + co];
+                            }
+            u16* dst = x->wtsb + (size_t)(l - 1) * BLKB_SZ;
+            HIPCHK(hipMemcpy(dst + WDB, hb.data(), 6 * C * C * 2, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(dst + WFB, hf.data(), 3 * C * C * 2, hipMemcpyHostToDevice));
             return 0;
         }
         if (!strcmp(tail, "biases")) { if ((rc = need(C))) return rc; return put(base + BD, host, C); }
@@ -412,9 +429,18 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                 for (int co = 0; co < C; ++co) tr[co * C + ci] = host[ci * C + co];
             if ((rc = put(base + WR, host, C * C))) return rc;
             if ((rc = put(base + WRT, tr.data(), C * C))) return rc;
-            std::vector<uint16_t> hb(2 * C * C);
+            std::vector<uint16_t> hb(2 * C * C), hf(C * C);
             for (size_t i = 0; i < C * C; ++i) { hb[i] = host_bf16(host[i]); hb[C * C + i] = host_bf16(tr[i]); }
-            HIPCHK(hipMemcpy(x->wtsb + (size_t)(l - 1) * BLKB_SZ + WRB, hb.data(), 2 * C * C * 2, hipMemcpyHostToDevice));
+            for (int q2 = 0; q2 < 4; ++q2)
+                for (int st = 0; st < 8; ++st)
+                    for (int ln = 0; ln < 64; ++ln)
+                        for (int e = 0; e < 8; ++e) {
+                            const int co = kperm(st, ln >> 5, e), co2 = 32 * q2 + (ln & 31);
+                            hf[(((size_t)q2 * 8 + st) * 64 + ln) * 8 + e] = hb[(size_t)co * C + co2];
+                        }
+            u16* dst = x->wtsb + (size_t)(l - 1) * BLKB_SZ;
+            HIPCHK(hipMemcpy(dst + WRB, hb.data(), 2 * C * C * 2, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(dst + WRFB, hf.data(), C * C * 2, hipMemcpyHostToDevice));
             return 0;
         }
         if (!strcmp(tail, "biases")) { if ((rc = need(C))) return rc; return put(base + BR, host, C); }

@@ -1,0 +1,353 @@
+// bf16 encoder block forward (precision 1): model.py:95-116 for one block,
+//   u = dconv_d(relu(e_l)) + b_d        (masked.py:110-160, K = 3, SAME zero padding)
+//   e_{l+1} = e_l + W_r^T relu(u) + b_r
+// with bf16 storage, v_mfma_f32_32x32x16_bf16 and fp32 accumulation.
+//
+// MI355X mapping ("column-owning" waves):
+//  * One 256-thread workgroup per CU (one wave per SIMD, up to 512 registers each), persistent
+//    over tiles of TMB = 128 positions in time_to_batch order (masked.py:57-86).  Wave w owns
+//    tile columns 32w..32w+31 and computes ALL 128 output channels of them, so nothing a wave
+//    produces is read by another wave: the only barrier per tile guards the input image.
+//  * Weights never leave the CU: W_d^T taps 0 and 2 sit in 256 registers as MFMA A fragments,
+//    tap 1 and W_r^T sit in LDS in fragment order (one conflict-free ds_read_b128 per fragment).
+//  * relu(u) never touches LDS: GEMM 1's fp32 accumulators are packed to bf16 and used directly
+//    as GEMM 2's B fragments.  GEMM 2's K (channel) order is permuted on the host to match the
+//    accumulator layout (WRF below).
+//  * Biases enter as the accumulators' initial values, the residual e_l as two MFMAs per
+//    32-channel tile against an identity fragment (exact: bf16 x 1.0 into fp32).
+//  * Input rows stream HBM -> LDS by global_load_lds (no VGPR staging), double-buffered: the
+//    next tile lands while this one computes.  Image rows are 272 B (256 + 16 pad), which makes
+//    the column-wise fragment reads conflict-free; the DMA fills the pad slot with a harmless
+//    re-read of the row's first chunk.
+//  * relu masks leave as 16-bit words in the accumulator layout (bit i = element i of one
+//    lane's 32x32 tile): u > 0 by this layer's position, e_{l+1} > 0 by the NEXT layer's
+//    position, so the backward applies them with no bit shuffling (block_bwd in
+//    encoder_bf16.hip).
+#include "common.h"
+#include <algorithm>
+
+namespace ast {
+namespace {
+
+constexpr int FT = 256;                  // threads: one wave per SIMD
+constexpr int RSB = 272;                 // image row stride (bytes)
+constexpr int FROWS = TMB + 8;           // max image rows (4 segments of 32 + 2 pads each)
+constexpr int NDMA = (FROWS * RSB + 1023) / 1024;   // 37 one-KiB DMA groups per image
+constexpr int BUFB = NDMA * 1024;        // bytes per image (tail slack absorbs the last group)
+constexpr int DPW = (NDMA + 3) / 4;      // DMA groups per wave
+
+struct FLayout {           // uniform per launch (see pick_flayout)
+    int M;                 // segment length; TMB = one segment with two halo rows
+    int nrows;             // image rows
+};
+
+__device__ __forceinline__ int frow(int c, const FLayout& ly) {   // image row of column c
+    return (c / ly.M) * (ly.M + 2) + 1 + (c % ly.M);
+}
+
+// time offset of image row L from the tile's base time (unmasked layouts):
+//   one segment: rows are positions p0-1 .. p0+128 of one sub-sequence, t = tb + (L-1) d
+//   segments of M = n: row (s, k) is position k-1 of sub-sequence j0 + s, t = tb + (k-1) d + s
+__device__ __forceinline__ int row_toff(int L, const FLayout& ly, int d) {
+    if (ly.M == TMB) return (L - 1) * d;
+    const int s = L / (ly.M + 2), k = L - s * (ly.M + 2);
+    return (k - 1) * d + s;
+}
+
+__device__ __forceinline__ uint4 relu8(uint4 v) {
+    return make_uint4(relu2(v.x), relu2(v.y), relu2(v.z), relu2(v.w));
+}
+
+__device__ __forceinline__ uint4 lds16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// 16 B per lane HBM -> LDS at lds_base + 16 * lane (global_load_lds_dwordx4).  Inline asm so the
+// compiler neither counts it nor drains it with vmcnt(0) before unrelated LDS reads: the kernel
+// waits for it explicitly (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void dma16(const void* src, uint32_t lds_base) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_base) : "memory");
+}
+
+// bit i of the result = (bf16 element i of the 8 packed dwords, as int16) > 0
+__device__ __forceinline__ uint32_t pos_bits16(const uint32_t (&pk)[8]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 7; k >= 0; --k) {
+        m = m + m + ((int)pk[k] >= 0x10000 ? 1u : 0u);          // high half > 0
+        m = m + m + ((short)(pk[k] & 0xffffu) > 0 ? 1u : 0u);   // low half > 0
+    }
+    return m;
+}
+
+template <bool MASKED>
+__global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
+    __shared__ __attribute__((aligned(16))) uint8_t XS[2][BUFB];   // e_l tile images
+    __shared__ __attribute__((aligned(16))) uint4 W1[4 * 8 * 64];  // W_d^T tap 1 A fragments
+    __shared__ __attribute__((aligned(16))) uint4 WRL[4 * 8 * 64]; // W_r^T A fragments (K permuted)
+    __shared__ __attribute__((aligned(16))) float BIAS[2 * C];     // b_d, b_r
+
+    const int tiles = a.T / TMB;
+    const int ntiles = a.B * tiles;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+
+    // ---- per-launch setup -------------------------------------------------------------
+    // taps 0 and 2 live in the accumulator register file (MFMA A operands may be AGPRs): the
+    // arch VGPRs stay free for accumulators, fragments and addresses
+    uint4 wr0[4][8], wr2[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int kb = 0; kb < 8; ++kb) {
+            const uint4* p0 = reinterpret_cast<const uint4*>(a.wf + ((size_t)((0 * 4 + q) * 8 + kb) * 64 + lane) * 8);
+            const uint4* p2 = reinterpret_cast<const uint4*>(a.wf + ((size_t)((2 * 4 + q) * 8 + kb) * 64 + lane) * 8);
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(wr0[q][kb]) : "v"(p0) : "memory");
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(wr2[q][kb]) : "v"(p2) : "memory");
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int i = tid; i < 4 * 8 * 64; i += FT) {
+        W1[i] = *reinterpret_cast<const uint4*>(a.wf + ((size_t)4 * 8 * 64 + i) * 8);
+        WRL[i] = *reinterpret_cast<const uint4*>(a.wrf + (size_t)i * 8);
+    }
+    if (tid < C) { BIAS[tid] = a.bd[tid]; BIAS[C + tid] = a.br[tid]; }
+    // identity A fragments: element e of lane (r, h) is 1 iff r == 16 sg + 8 h + e
+    uint4 idf[2];
+#pragma unroll
+    for (int sg = 0; sg < 2; ++sg) {
+        const int e = r - 16 * sg - 8 * h;
+        uint32_t dw[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            dw[k] = (e == 2 * k ? 0x3f80u : 0u) | (e == 2 * k + 1 ? 0x3f800000u : 0u);
+        idf[sg] = make_uint4(dw[0], dw[1], dw[2], dw[3]);
+    }
+
+    const int c = 32 * w + r;                  // this lane's tile column
+    const int Lc = frow(c, ly);
+    const int tcoff = MASKED ? 0 : row_toff(Lc, ly, a.d);
+
+    // DMA slots: group g = w + 4 j covers image bytes [1024 g, 1024 g + 1024); this lane's
+    // 16 B land at row L, chunk qc (qc == 16: the pad slot, filled from chunk 0)
+    int soff[DPW];       // source element offset from the tile's base row (unmasked layouts)
+    int scls[DPW];       // source class: 0 row, 1 zero, 2 left halo, 3 right halo
+    int srow[DPW], schk[DPW];
+#pragma unroll
+    for (int j = 0; j < DPW; ++j) {
+        const int g = w + 4 * j;
+        const int o = g * 1024 + lane * 16;
+        const int L = o / RSB, qc = (o - L * RSB) >> 4;
+        const int ch = qc < 16 ? qc : 0;
+        srow[j] = L;
+        schk[j] = ch;
+        int cls = 0;
+        if (L >= ly.nrows) cls = 1;
+        else if (ly.M == TMB) cls = L == 0 ? 2 : (L == TMB + 1 ? 3 : 0);
+        else {
+            const int k = L % (ly.M + 2);
+            cls = (k == 0 || k == ly.M + 1) ? 1 : 0;
+        }
+        scls[j] = cls;
+        soff[j] = MASKED || cls == 1 ? 0 : row_toff(L, ly, a.d) * C + ch * 8;
+    }
+    __syncthreads();
+
+    auto stage = [&](int tl, int buf) {
+        tl = tl < ntiles ? tl : ntiles - 1;    // past the end: re-load a valid tile (unused)
+        const int b = tl / tiles, p0 = (tl - b * tiles) * TMB;
+        const u16* clip = a.ein + (size_t)b * a.T * C;
+        const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[buf][0] + (uint32_t)(w * 1024);
+        if (MASKED) {
+#pragma unroll
+            for (int j = 0; j < DPW; ++j) {
+                if (w + 4 * j >= NDMA) break;
+                const int p = p0 + srow[j] - 1;
+                const u16* src = a.zero;
+                if (scls[j] != 1 && p >= 0 && p < a.T)
+                    src = clip + (size_t)((p % a.n) * a.d + p / a.n) * C + schk[j] * 8;
+                dma16(src, lds0 + j * 4096);
+            }
+        } else {
+            int m0 = 0, tb;
+            if (ly.M == TMB) { m0 = p0 % a.n; tb = m0 * a.d + p0 / a.n; }
+            else tb = p0 / a.n;
+            // valid classes: bit k set = class k loads a row this tile
+            const uint32_t vmask = 1u | (m0 > 0 ? 4u : 0u) | (m0 + TMB < a.n ? 8u : 0u);
+            const u16* base = clip + (size_t)tb * C;
+#pragma unroll
+            for (int j = 0; j < DPW; ++j) {
+                if (w + 4 * j >= NDMA) break;
+                const u16* src = ((vmask >> scls[j]) & 1u) ? base + soff[j] : a.zero;
+                dma16(src, lds0 + j * 4096);
+            }
+        }
+    };
+
+    stage(blockIdx.x, 0);
+    int it = 0;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
+        const int cur = it & 1;
+        const int b = tile / tiles, p0 = (tile - b * tiles) * TMB;
+        // this wave's DMA of the current image is complete (at most the 9 or 10 stores of the
+        // previous tile, issued after it, may still be in flight: vmcnt counts in issue order);
+        // the barrier makes every wave's part visible and guarantees the other image is no
+        // longer read
+        if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        stage(tile + gridDim.x, cur ^ 1);
+
+        int tcol;                               // time of this lane's column
+        bool ok0 = true, ok2 = true;
+        if (MASKED) {
+            const int p = p0 + c, m = p % a.n;
+            tcol = m * a.d + p / a.n;
+            ok0 = m > 0;
+            ok2 = m < a.n - 1;
+        } else {
+            const int tb = ly.M == TMB ? (p0 % a.n) * a.d + p0 / a.n : p0 / a.n;
+            tcol = tb + tcoff;
+        }
+        const uint8_t* xb = &XS[cur][(Lc - 1) * RSB + h * 16];   // tap-0 row, this lane's half
+
+        // ---- GEMM 1 (dilated conv): 24 (tap, K-block) steps x 4 output-channel tiles ----
+        // B fragment of step st: relu(e) of row (column + tap - 1), K-block kb; loaded two steps
+        // ahead (LDS latency is covered by the 4 MFMAs of each step), tap-1 A fragments one
+        // step ahead.
+        f32x16 acc[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 b4 = *reinterpret_cast<const float4*>(&BIAS[32 * q + 8 * g + 4 * h]);
+                acc[q][4 * g + 0] = b4.x; acc[q][4 * g + 1] = b4.y;
+                acc[q][4 * g + 2] = b4.z; acc[q][4 * g + 3] = b4.w;
+            }
+        {
+            auto bload = [&](int st) { return lds16(xb + (st >> 3) * RSB + (st & 7) * 32); };
+            uint4 bl[3], al[2][4];
+            bl[0] = bload(0);
+            bl[1] = bload(1);
+#pragma unroll
+            for (int st = 0; st < 24; ++st) {
+                const int tp = st >> 3, kb = st & 7;
+                if (st + 2 < 24) bl[(st + 2) % 3] = bload(st + 2);
+                if (st + 1 >= 8 && st + 1 < 16) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) al[(st + 1) & 1][q] = W1[(q * 8 + ((st + 1) & 7)) * 64 + lane];
+                }
+                uint4 bv = relu8(bl[st % 3]);
+                if (MASKED && ((tp == 0 && !ok0) || (tp == 2 && !ok2))) bv = make_uint4(0, 0, 0, 0);
+                if (tp == 0) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[q] = mfma_bf16(wr0[q][kb], bv, acc[q]);
+                } else if (tp == 1) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[q] = mfma_bf16(al[st & 1][q], bv, acc[q]);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[q] = mfma_bf16(wr2[q][kb], bv, acc[q]);
+                }
+                __builtin_amdgcn_sched_barrier(0);   // keep the prefetch distance
+            }
+        }
+        // ---- epilogue 1: relu(u) (bias is in the accumulator) -> bf16 B fragments; u > 0 bits
+        uint4 vf[4][2];
+        uint32_t mub[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t pk[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pk[k] = relu2(pack2(acc[q][2 * k], acc[q][2 * k + 1]));
+            vf[q][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            vf[q][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+            mub[q] = pos_bits16(pk);
+        }
+        // u > 0 bits by this layer's position: lane (r, h) -> words [h][0..3]
+        *reinterpret_cast<uint2*>(a.mu + ((size_t)b * a.T + p0 + c) * 8 + 4 * h) =
+            make_uint2(mub[0] | (mub[1] << 16), mub[2] | (mub[3] << 16));
+
+        // ---- GEMM 2 (1x1) + bias + residual ----
+        f32x16 acc2[4];
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 b4 = *reinterpret_cast<const float4*>(&BIAS[C + 32 * q2 + 8 * g + 4 * h]);
+                acc2[q2][4 * g + 0] = b4.x; acc2[q2][4 * g + 1] = b4.y;
+                acc2[q2][4 * g + 2] = b4.z; acc2[q2][4 * g + 3] = b4.w;
+            }
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+            for (int q2 = 0; q2 < 4; ++q2)
+                acc2[q2] = mfma_bf16(WRL[(q2 * 8 + s) * 64 + lane], vf[s >> 1][s & 1], acc2[q2]);
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2)
+#pragma unroll
+            for (int sg = 0; sg < 2; ++sg)
+                acc2[q2] = mfma_bf16(idf[sg], lds16(xb + RSB + (2 * q2 + sg) * 32), acc2[q2]);
+
+        // ---- epilogue 2: bf16 rows out (two 16-B pieces per lane pair), e_{l+1} > 0 bits ----
+        u16* orow = a.eout + ((size_t)b * a.T + tcol) * C;
+        uint32_t meb[4];
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) {
+            uint32_t o[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o[k] = pack2(acc2[q2][2 * k], acc2[q2][2 * k + 1]);
+            meb[q2] = pos_bits16(o);
+#pragma unroll
+            for (int g = 0; g < 4; g += 2) {
+                // lanes h = 0 hold channels 8g..8g+3 (o[2g], o[2g+1]), h = 1 hold 8g+4..8g+7:
+                // swap so h = 0 holds group g whole and h = 1 group g+1 (guide T21)
+                uint32_t ax = o[2 * g], ay = o[2 * g + 1], bx = o[2 * g + 2], by = o[2 * g + 3];
+                auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+                auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+                ax = sx[0]; bx = sx[1]; ay = sy[0]; by = sy[1];
+                *reinterpret_cast<uint4*>(orow + 32 * q2 + 8 * g + 8 * h) = make_uint4(ax, ay, bx, by);
+            }
+        }
+        if (a.me_next) {
+            const int pn = (tcol & ((1 << a.dn_log2) - 1)) * a.nn + (tcol >> a.dn_log2);
+            *reinterpret_cast<uint2*>(a.me_next + ((size_t)b * a.T + pn) * 8 + 4 * h) =
+                make_uint2(meb[0] | (meb[1] << 16), meb[2] | (meb[3] << 16));
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int g_cus_c = 0;
+int num_cus_c() {
+    if (!g_cus_c) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_cus_c, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_cus_c <= 0) g_cus_c = 256;
+    }
+    return g_cus_c;
+}
+
+// Segment layout when a tile lies inside one sub-sequence (n % 128 == 0) or holds whole
+// sub-sequences of >= 32 positions; otherwise one segment with per-column tap masks.
+bool pick_flayout(int n, FLayout& ly) {
+    if (n % TMB == 0) { ly.M = TMB; ly.nrows = TMB + 2; return false; }
+    if (n < TMB && TMB % n == 0 && n >= 32) { ly.M = n; ly.nrows = (TMB / n) * (n + 2); return false; }
+    ly.M = TMB; ly.nrows = TMB + 2;
+    return true;
+}
+
+}  // namespace
+
+void launch_block_fwd_c(const FwdArgsC& a, hipStream_t s) {
+    const int nt = a.B * (a.T / TMB);
+    const dim3 grid(std::min(nt, num_cus_c()));
+    FLayout ly;
+    if (pick_flayout(a.n, ly)) hipLaunchKernelGGL(k_block_fwd_c<true>, grid, dim3(FT), 0, s, a, ly);
+    else hipLaunchKernelGGL(k_block_fwd_c<false>, grid, dim3(FT), 0, s, a, ly);
+}
+
+}  // namespace ast

@@ -6,8 +6,11 @@
 //                           group (fp32).  Tapped tensors are overwritten in place by their
 //                           direct loss gradient D during the Gram backward.
 //   mu/me [NB][B][T][4]     u>0 / e_l>0 relu masks, one bit per channel (16 B per row);
-//                           fp32 kernels index them by time, bf16 kernels by the layer's
-//                           time_to_batch position (a tile's masks are one contiguous run)
+//                           fp32 kernels index them by time, channel c at bit c.  bf16 kernels
+//                           index them by the layer's time_to_batch position (a tile's masks
+//                           are one contiguous run) as u16 words [h][q] in the 32x32 MFMA
+//                           accumulator layout: bit i of word (h, q) is channel
+//                           32 q + (i & 3) + 8 (i >> 2) + 4 h
 //   chain [2][B][T][C]      fp32 backward ping-pong (d loss / d e_l)
 // Dilated rows are visited in time_to_batch order (masked.py:57-86): tile position p maps to
 // time t = (p % n) * d + p / n with n = T / d, so a tile's tap neighbours are p-1 / p+1 and
@@ -42,9 +45,10 @@ constexpr int GCB = 32;       // Gram: channels per workgroup
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((uint32_t)v << 16); }
 __device__ __forceinline__ float bflo(uint32_t v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ float bfhi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
-__device__ __forceinline__ uint32_t pack2(float a, float b) {   // RNE, v_cvt_pk_bf16_f32
-    bf16x2 v = {(__bf16)a, (__bf16)b};
-    return __builtin_bit_cast(uint32_t, v);
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack2(float a, float b) {   // RNE, one v_cvt_pk_bf16_f32
+    const f32x2 x = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(x, bf16x2));
 }
 __device__ __forceinline__ u16 f2bf(float a) { return (u16)(pack2(a, 0.f) & 0xffffu); }
 __device__ __forceinline__ uint32_t relu2(uint32_t u) {         // bf16 relu == int16 max(v, 0)
@@ -96,6 +100,19 @@ struct BwdArgsB {
     const u16* wd;     // [3][ci][co] bf16 (A operand of step 2)
     const uint32_t* mu; const uint32_t* me;
     int B, T, d, n;
+};
+
+// column-owning bf16 block forward (block_fwd_bf16.hip)
+struct FwdArgsC {
+    const u16* ein; u16* eout;
+    const u16* wf;         // [3 taps][4 q][8 kb][64 lanes][8] W_d^T A fragments
+    const u16* wrf;        // [4 q2][8 s][64][8] W_r^T A fragments, K in accumulator order
+    const float* bd; const float* br;
+    uint16_t* mu;          // [B*T][2 h][4 q] u > 0 bits, this layer's positions
+    uint16_t* me_next;     // [B*T][2][4] e_{l+1} > 0 bits, the next layer's positions (or null)
+    const u16* zero;       // >= 256 zero bytes
+    int B, T, d, n;        // dilation, n = T / d
+    int dn_log2, nn;       // next layer: log2 dilation, T / dilation
 };
 
 struct GramArgs {
@@ -155,7 +172,7 @@ struct ContentArgs {
 // launchers (encoder.hip / gram.hip / optim.hip)
 template <typename S>
 void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b0,
-                          int B, int T, hipStream_t s);
+                          int B, int T, hipStream_t s, uint16_t* me0 = nullptr);
 template <typename S>
 void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T,
                           hipStream_t s);
@@ -163,6 +180,7 @@ void launch_block_fwd(const FwdArgs& a, hipStream_t s);
 void launch_block_bwd(const BwdArgs& a, hipStream_t s);
 void launch_block_fwd_bf16(const FwdArgsB& a, hipStream_t s);
 void launch_block_bwd_bf16(const BwdArgsB& a, hipStream_t s);
+void launch_block_fwd_c(const FwdArgsC& a, hipStream_t s);
 template <typename S>
 void launch_bottleneck_fwd(const S* e, float* y, const float* wb, const float* bb,
                            int B, int T, hipStream_t s);

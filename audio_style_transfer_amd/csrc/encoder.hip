@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
                                                        S* __restrict__ e0,
                                                        const float* __restrict__ w0,
                                                        const float* __restrict__ b0, int B,
-                                                       int T) {
+                                                       int T, uint16_t* __restrict__ me0) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;   // (row, float4)
     const size_t rowi = i >> 5;
     if (rowi >= (size_t)B * T) return;
@@ -248,7 +248,19 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
     if constexpr (sizeof(S) == 4) {
         *reinterpret_cast<float4*>(e0 + rowi * C + q * 4) = make_float4(o[0], o[1], o[2], o[3]);
     } else {
-        *reinterpret_cast<uint2*>(e0 + rowi * C + q * 4) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+        const uint32_t p0 = pack2(o[0], o[1]), p1 = pack2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(e0 + rowi * C + q * 4) = make_uint2(p0, p1);
+        if (me0) {
+            // e_0 > 0 bits for block 0's backward (dilation 1: position = time), in the MFMA
+            // accumulator layout of block_fwd_bf16.hip: channels 4q..4q+3 = 32 Q + 8 g + 4 h + j
+            // with q = 8 Q + 2 g + h are bits 4g..4g+3 of word (h, Q)
+            uint32_t nib = ((short)(p0 & 0xffffu) > 0 ? 1u : 0u) | ((int)p0 >= 0x10000 ? 2u : 0u) |
+                           ((short)(p1 & 0xffffu) > 0 ? 4u : 0u) | ((int)p1 >= 0x10000 ? 8u : 0u);
+            nib <<= 4 * ((q >> 1) & 3);
+            nib |= (uint32_t)__shfl_xor((int)nib, 2);
+            nib |= (uint32_t)__shfl_xor((int)nib, 4);
+            if (((q >> 1) & 3) == 0) me0[rowi * 8 + (q & 1) * 4 + (q >> 3)] = (uint16_t)nib;
+        }
     }
 }
 
@@ -331,10 +343,10 @@ void launch_block_bwd(const BwdArgs& a, hipStream_t s) {
 }
 template <typename S>
 void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b0, int B, int T,
-                          hipStream_t s) {
+                          hipStream_t s, uint16_t* me0) {
     const size_t n = (size_t)B * T * 32;
     hipLaunchKernelGGL(k_startconv_fwd<S>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x,
-                       e0, w0, b0, B, T);
+                       e0, w0, b0, B, T, me0);
 }
 template <typename S>
 void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T, hipStream_t s) {
@@ -359,8 +371,8 @@ void launch_bottleneck_bwd(const float* gy, S* ge, const float* wb, int accumula
 void launch_to_f32(const u16* src, float* dst, size_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_to_f32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, n);
 }
-template void launch_startconv_fwd<float>(const float*, float*, const float*, const float*, int, int, hipStream_t);
-template void launch_startconv_fwd<u16>(const float*, u16*, const float*, const float*, int, int, hipStream_t);
+template void launch_startconv_fwd<float>(const float*, float*, const float*, const float*, int, int, hipStream_t, uint16_t*);
+template void launch_startconv_fwd<u16>(const float*, u16*, const float*, const float*, int, int, hipStream_t, uint16_t*);
 template void launch_startconv_bwd<float>(const float*, float*, const float*, int, int, hipStream_t);
 template void launch_startconv_bwd<u16>(const u16*, float*, const float*, int, int, hipStream_t);
 template void launch_bottleneck_fwd<float>(const float*, float*, const float*, const float*, int, int, hipStream_t);

@@ -494,10 +494,10 @@ __global__ void __launch_bounds__(NTH, 1) k_block_bwd_bf16(BwdArgsB a, Layout ly
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const uint32_t mw = MU[Lc[j] * 4 + (w & 3)];
+            const uint32_t mw = reinterpret_cast<const uint16_t*>(MU)[Lc[j] * 8 + h * 4 + (w & 3)];
             float v[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = ((mw >> acc_row(i, h)) & 1u) ? acc[j][i] : 0.f;
+            for (int i = 0; i < 16; ++i) v[i] = ((mw >> i) & 1u) ? acc[j][i] : 0.f;
 #pragma unroll
             for (int g = 0; g < 4; ++g)
                 *reinterpret_cast<uint2*>(&U[Lc[j] * XSB + cb + 8 * g + 4 * h]) =
@@ -516,10 +516,10 @@ __global__ void __launch_bounds__(NTH, 1) k_block_bwd_bf16(BwdArgsB a, Layout ly
                 hacc = mfma_bf16(av, bv, hacc);
             }
             if (r < 2) {
-                const uint32_t mw = TT[hrow] >= 0 ? MU[hrow * 4 + (w & 3)] : 0u;
+                const uint32_t mw = TT[hrow] >= 0 ? reinterpret_cast<const uint16_t*>(MU)[hrow * 8 + h * 4 + (w & 3)] : 0u;
                 float v[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] = ((mw >> acc_row(i, h)) & 1u) ? hacc[i] : 0.f;
+                for (int i = 0; i < 16; ++i) v[i] = ((mw >> i) & 1u) ? hacc[i] : 0.f;
 #pragma unroll
                 for (int g = 0; g < 4; ++g)
                     *reinterpret_cast<uint2*>(&U[hrow * XSB + cb + 8 * g + 4 * h]) =
@@ -565,12 +565,12 @@ __global__ void __launch_bounds__(NTH, 1) k_block_bwd_bf16(BwdArgsB a, Layout ly
         // epilogue: g_l = tot + [e_l > 0] gh, over this wave's channels of G in place
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const uint32_t mw = ME[Lc[j] * 4 + (w & 3)];
+            const uint32_t mw = reinterpret_cast<const uint16_t*>(ME)[Lc[j] * 8 + h * 4 + (w & 3)];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 uint2* pgp = reinterpret_cast<uint2*>(&G[Lc[j] * XSB + cb + 8 * g + 4 * h]);
                 const uint2 tv = *pgp;
-                const int Rr = 8 * g + 4 * h;
+                const int Rr = 4 * g;   // element index of channel cb + 8 g + 4 h
                 const float o0 = bflo(tv.x) + (((mw >> (Rr + 0)) & 1u) ? acc[j][4 * g + 0] : 0.f);
                 const float o1 = bfhi(tv.x) + (((mw >> (Rr + 1)) & 1u) ? acc[j][4 * g + 1] : 0.f);
                 const float o2 = bflo(tv.y) + (((mw >> (Rr + 2)) & 1u) ? acc[j][4 * g + 2] : 0.f);
