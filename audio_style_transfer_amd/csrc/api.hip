@@ -218,6 +218,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
         uint32_t* me = x->me + (size_t)l * c.batch * c.T * 4;
         if (x->bf) {
             FwdArgsC a;
+            a.stamps = g_stamps;
             u16* wb = blkwb(x, l);
             a.ein = (const u16*)tens(x, l); a.eout = (u16*)tens(x, l + 1);
             a.wf = wb + WFB; a.wrf = wb + WRFB; a.bd = w + BD; a.br = w + BR;

@@ -19,15 +19,18 @@
 //    next tile lands while this one computes.  Image rows are 272 B (256 + 16 pad), which makes
 //    the column-wise fragment reads conflict-free; the DMA fills the pad slot with a harmless
 //    re-read of the row's first chunk.
-//  * relu masks leave as 16-bit words in the accumulator layout (bit i = element i of one
-//    lane's 32x32 tile): u > 0 by this layer's position, e_{l+1} > 0 by the NEXT layer's
+//  * relu masks leave as 16-bit words in the accumulator layout (bit mbit(i) = element i of one
+//    lane's 32x32 tile, common.h): u > 0 by this layer's position, e_{l+1} > 0 by the NEXT layer's
 //    position, so the backward applies them with no bit shuffling (block_bwd in
 //    encoder_bf16.hip).
 #include "common.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace ast {
 namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int FT = 256;                  // threads: one wave per SIMD
 constexpr int RSB = 272;                 // image row stride (bytes)
@@ -70,23 +73,13 @@ __device__ __forceinline__ void dma16(const void* src, uint32_t lds_base) {
                  : "=&s"(keep) : "v"(src), "s"(lds_base) : "memory");
 }
 
-// bit i of the result = (bf16 element i of the 8 packed dwords, as int16) > 0
-__device__ __forceinline__ uint32_t pos_bits16(const uint32_t (&pk)[8]) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int k = 7; k >= 0; --k) {
-        m = m + m + ((int)pk[k] >= 0x10000 ? 1u : 0u);          // high half > 0
-        m = m + m + ((short)(pk[k] & 0xffffu) > 0 ? 1u : 0u);   // low half > 0
-    }
-    return m;
-}
-
 template <bool MASKED>
 __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
     __shared__ __attribute__((aligned(16))) uint8_t XS[2][BUFB];   // e_l tile images
     __shared__ __attribute__((aligned(16))) uint4 W1[4 * 8 * 64];  // W_d^T tap 1 A fragments
     __shared__ __attribute__((aligned(16))) uint4 WRL[4 * 8 * 64]; // W_r^T A fragments (K permuted)
     __shared__ __attribute__((aligned(16))) float BIAS[2 * C];     // b_d, b_r
+    __shared__ __attribute__((aligned(16))) uint8_t STG[4][16 * RSB]; // output staging, per wave
 
     const int tiles = a.T / TMB;
     const int ntiles = a.B * tiles;
@@ -96,18 +89,21 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
 
     // ---- per-launch setup -------------------------------------------------------------
     // taps 0 and 2 live in the accumulator register file (MFMA A operands may be AGPRs): the
-    // arch VGPRs stay free for accumulators, fragments and addresses
+    // arch VGPRs stay free for accumulators, fragments and addresses.  Plain loads (the compiler
+    // counts them), then a tied no-op asm that pins each fragment to AGPRs.
     uint4 wr0[4][8], wr2[4][8];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int kb = 0; kb < 8; ++kb) {
-            const uint4* p0 = reinterpret_cast<const uint4*>(a.wf + ((size_t)((0 * 4 + q) * 8 + kb) * 64 + lane) * 8);
-            const uint4* p2 = reinterpret_cast<const uint4*>(a.wf + ((size_t)((2 * 4 + q) * 8 + kb) * 64 + lane) * 8);
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(wr0[q][kb]) : "v"(p0) : "memory");
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=a"(wr2[q][kb]) : "v"(p2) : "memory");
+            const uint4 v0 = *reinterpret_cast<const uint4*>(a.wf + ((size_t)((0 * 4 + q) * 8 + kb) * 64 + lane) * 8);
+            const uint4 v2 = *reinterpret_cast<const uint4*>(a.wf + ((size_t)((2 * 4 + q) * 8 + kb) * 64 + lane) * 8);
+            u32x4 t0 = __builtin_bit_cast(u32x4, v0), t2 = __builtin_bit_cast(u32x4, v2);
+            asm volatile("" : "=a"(t0) : "0"(t0));
+            asm volatile("" : "=a"(t2) : "0"(t2));
+            wr0[q][kb] = __builtin_bit_cast(uint4, t0);
+            wr2[q][kb] = __builtin_bit_cast(uint4, t2);
         }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int i = tid; i < 4 * 8 * 64; i += FT) {
         W1[i] = *reinterpret_cast<const uint4*>(a.wf + ((size_t)4 * 8 * 64 + i) * 8);
         WRL[i] = *reinterpret_cast<const uint4*>(a.wrf + (size_t)i * 8);
@@ -154,70 +150,164 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
     }
     __syncthreads();
 
-    auto stage = [&](int tl, int buf) {
-        tl = tl < ntiles ? tl : ntiles - 1;    // past the end: re-load a valid tile (unused)
+    auto stage = [&](int tl, int buf) {          // DMA of a whole tile image (prologue)
         const int b = tl / tiles, p0 = (tl - b * tiles) * TMB;
-        const u16* clip = a.ein + (size_t)b * a.T * C;
-        const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[buf][0] + (uint32_t)(w * 1024);
-        if (MASKED) {
-#pragma unroll
-            for (int j = 0; j < DPW; ++j) {
-                if (w + 4 * j >= NDMA) break;
-                const int p = p0 + srow[j] - 1;
-                const u16* src = a.zero;
-                if (scls[j] != 1 && p >= 0 && p < a.T)
-                    src = clip + (size_t)((p % a.n) * a.d + p / a.n) * C + schk[j] * 8;
-                dma16(src, lds0 + j * 4096);
-            }
-        } else {
-            int m0 = 0, tb;
+        int m0 = 0, tb = 0;
+        if (!MASKED) {
             if (ly.M == TMB) { m0 = p0 % a.n; tb = m0 * a.d + p0 / a.n; }
             else tb = p0 / a.n;
-            // valid classes: bit k set = class k loads a row this tile
-            const uint32_t vmask = 1u | (m0 > 0 ? 4u : 0u) | (m0 + TMB < a.n ? 8u : 0u);
-            const u16* base = clip + (size_t)tb * C;
+        }
+        const uint32_t vmask = 1u | (!MASKED && ly.M == TMB && m0 > 0 ? 4u : 0u) |
+                               (!MASKED && ly.M == TMB && m0 + TMB < a.n ? 8u : 0u);
+        const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[buf][0] + (uint32_t)(w * 1024);
 #pragma unroll
-            for (int j = 0; j < DPW; ++j) {
-                if (w + 4 * j >= NDMA) break;
-                const u16* src = ((vmask >> scls[j]) & 1u) ? base + soff[j] : a.zero;
-                dma16(src, lds0 + j * 4096);
+        for (int j = 0; j < DPW; ++j) {
+            if (w + 4 * j >= NDMA) break;
+            const u16* src = a.zero;
+            if (MASKED) {
+                const int p = p0 + srow[j] - 1;
+                if (scls[j] != 1 && p >= 0 && p < a.T)
+                    src = a.ein + ((size_t)b * a.T + (p % a.n) * a.d + p / a.n) * C + schk[j] * 8;
+            } else if ((vmask >> scls[j]) & 1u) {
+                src = a.ein + ((size_t)b * a.T + tb) * C + soff[j];
             }
+            dma16(src, lds0 + j * 4096);
+        }
+    };
+
+    // staged output rows: this lane's (round rho, piece k) row is wave column 16 rho + 4 k + lane/16
+    int otoff[2][4];
+#pragma unroll
+    for (int rho = 0; rho < 2; ++rho)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            otoff[rho][k] = MASKED ? 0 : row_toff(frow(32 * w + 16 * rho + 4 * k + (lane >> 4), ly), ly, a.d);
+    uint8_t* stg = &STG[w][0];
+
+    // ---- per-tile geometry ----------------------------------------------------------------
+    struct Tile { int b, p0, tb; };
+    auto tile_at = [&](int tl) {
+        Tile t;
+        t.b = tl / tiles;
+        t.p0 = (tl - t.b * tiles) * TMB;
+        t.tb = MASKED ? 0 : (ly.M == TMB ? (t.p0 % a.n) * a.d + t.p0 / a.n : t.p0 / a.n);
+        return t;
+    };
+    auto col_time = [&](const Tile& t, int cc, int toff) {   // time of tile column cc
+        if (MASKED) {
+            const int p = t.p0 + cc;
+            return (p % a.n) * a.d + p / a.n;
+        }
+        return t.tb + toff;
+    };
+
+    // ---- epilogue 2 pieces (run for the PREVIOUS tile while this tile's GEMM 1 runs) ------
+    // chunk(q2): bf16 pack, e_{l+1} > 0 bits, half-wave swap (guide T21): afterwards lane (n, h)
+    // holds 16-B chunks 4 q2 + 2 gp + h (gp = 0, 1) of row n
+    auto epi2_chunk = [&](const f32x16& acc2q, uint4 (&opk)[2], uint32_t& mebq) {
+        uint32_t o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = pack2(acc2q[2 * k], acc2q[2 * k + 1]);
+        mebq = pos_bits16(o);
+#pragma unroll
+        for (int gp = 0; gp < 2; ++gp) {
+            const int g = 2 * gp;
+            uint32_t ax = o[2 * g], ay = o[2 * g + 1], bx = o[2 * g + 2], by = o[2 * g + 3];
+            auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+            auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+            opk[gp] = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+        }
+    };
+    // round rho: rows 16 rho .. 16 rho + 15 of this wave go through the staging rows and leave
+    // as whole 256-B rows (16 lanes per row)
+    // The staging rows are written by half the lanes and read by all: a wave-scope fence keeps
+    // the compiler from hoisting one lane's read above another lane's write (or sinking a
+    // write above a read), which per-thread program order alone does not forbid.
+    auto wave_fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
+    auto epi2_stage = [&](int rho, const uint4 (&opk)[4][2]) {
+        wave_fence();
+        if ((r >> 4) == rho) {
+#pragma unroll
+            for (int q2 = 0; q2 < 4; ++q2)
+#pragma unroll
+                for (int gp = 0; gp < 2; ++gp)
+                    *reinterpret_cast<uint4*>(stg + (r & 15) * RSB + (4 * q2 + 2 * gp + h) * 16) = opk[q2][gp];
+        }
+        wave_fence();
+    };
+    auto epi2_store = [&](int rho, const Tile& t) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = lds16(stg + (4 * k + (lane >> 4)) * RSB + (lane & 15) * 16);
+            const int tt = col_time(t, 32 * w + 16 * rho + 4 * k + (lane >> 4), otoff[rho][k]);
+            *reinterpret_cast<uint4*>(a.eout + ((size_t)t.b * a.T + tt) * C + (lane & 15) * 8) = v;
+        }
+    };
+    auto me_store = [&](const Tile& t, const uint32_t (&meb)[4]) {
+        if (a.me_next) {
+            const int tc = col_time(t, c, tcoff);
+            const int pn = (tc & ((1 << a.dn_log2) - 1)) * a.nn + (tc >> a.dn_log2);
+            *reinterpret_cast<uint2*>(a.me_next + ((size_t)t.b * a.T + pn) * 8 + 4 * h) =
+                make_uint2(meb[0] | (meb[1] << 16), meb[2] | (meb[3] << 16));
         }
     };
 
     stage(blockIdx.x, 0);
+    f32x16 acc[4];                  // GEMM 1 accumulators
+    f32x16 acc2[4];                 // GEMM 2 accumulators, carried into the next iteration
+    Tile prev{0, 0, 0};
     int it = 0;
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
+    STAMP_DECL
+
+    // One tile per iteration, two phases:
+    //  A: GEMM 1 of this tile (24 steps x 4 MFMA) with, spread over its 8 windows of 3 steps,
+    //     epilogue 2 + stores of the previous tile and the DMA of the next tile
+    //  B: epilogue 1 of this tile interleaved with its GEMM 2 (10 steps x 4 MFMA)
+    auto body = [&](auto has_prev, int tile) {
+        constexpr bool PREV = decltype(has_prev)::value;
         const int cur = it & 1;
-        const int b = tile / tiles, p0 = (tile - b * tiles) * TMB;
-        // this wave's DMA of the current image is complete (at most the 9 or 10 stores of the
+        const Tile cu = tile_at(tile);
+        // this wave's DMA of the current image is complete (only the <= 10 stores of the
         // previous tile, issued after it, may still be in flight: vmcnt counts in issue order);
-        // the barrier makes every wave's part visible and guarantees the other image is no
-        // longer read
-        if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        // the barrier publishes every wave's part and retires all reads of the other image
+        if (PREV) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        stage(tile + gridDim.x, cur ^ 1);
+        STAMP(0)
 
-        int tcol;                               // time of this lane's column
         bool ok0 = true, ok2 = true;
         if (MASKED) {
-            const int p = p0 + c, m = p % a.n;
-            tcol = m * a.d + p / a.n;
+            const int m = (cu.p0 + c) % a.n;
             ok0 = m > 0;
             ok2 = m < a.n - 1;
-        } else {
-            const int tb = ly.M == TMB ? (p0 % a.n) * a.d + p0 / a.n : p0 / a.n;
-            tcol = tb + tcoff;
         }
         const uint8_t* xb = &XS[cur][(Lc - 1) * RSB + h * 16];   // tap-0 row, this lane's half
 
-        // ---- GEMM 1 (dilated conv): 24 (tap, K-block) steps x 4 output-channel tiles ----
-        // B fragment of step st: relu(e) of row (column + tap - 1), K-block kb; loaded two steps
-        // ahead (LDS latency is covered by the 4 MFMAs of each step), tap-1 A fragments one
-        // step ahead.
-        f32x16 acc[4];
+        // next tile's DMA: source pointers of the wave's slots
+        const int ntl = tile + gridDim.x < ntiles ? tile + gridDim.x : ntiles - 1;
+        const Tile nx = tile_at(ntl);
+        const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[cur ^ 1][0] + (uint32_t)(w * 1024);
+        uint32_t vmask = 1u;
+        if (!MASKED && ly.M == TMB) {
+            const int m0 = nx.p0 % a.n;
+            vmask |= (m0 > 0 ? 4u : 0u) | (m0 + TMB < a.n ? 8u : 0u);
+        }
+        const u16* nbase = a.ein + ((size_t)nx.b * a.T + nx.tb) * C;
+        auto dma_slot = [&](int j) {
+            if (w + 4 * j >= NDMA) return;
+            const u16* src = a.zero;
+            if (MASKED) {
+                const int p = nx.p0 + srow[j] - 1;
+                if (scls[j] != 1 && p >= 0 && p < a.T)
+                    src = a.ein + ((size_t)nx.b * a.T + (p % a.n) * a.d + p / a.n) * C + schk[j] * 8;
+            } else if ((vmask >> scls[j]) & 1u) {
+                src = nbase + soff[j];
+            }
+            dma16(src, lds0 + j * 4096);
+        };
+
+        // ---- phase A ----
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -226,6 +316,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
                 acc[q][4 * g + 0] = b4.x; acc[q][4 * g + 1] = b4.y;
                 acc[q][4 * g + 2] = b4.z; acc[q][4 * g + 3] = b4.w;
             }
+        uint4 opk[4][2];
+        uint32_t meb[4];
         {
             auto bload = [&](int st) { return lds16(xb + (st >> 3) * RSB + (st & 7) * 32); };
             uint4 bl[3], al[2][4];
@@ -251,27 +343,35 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) acc[q] = mfma_bf16(wr2[q][kb], bv, acc[q]);
                 }
-                __builtin_amdgcn_sched_barrier(0);   // keep the prefetch distance
+                // side work of window st / 3, placed in its last step
+                if (st % 3 == 2) {
+                    const int win = st / 3;
+                    if (win < 5) { dma_slot(2 * win); dma_slot(2 * win + 1); }
+                    if (PREV) {
+                        if (win < 4) epi2_chunk(acc2[win], opk[win], meb[win]);
+                        if (win == 4) me_store(prev, meb);
+#ifdef DBG_NOSTAGE
+                        if (win == 5) {
+                            u16* orow = a.eout + ((size_t)prev.b * a.T + col_time(prev, c, tcoff)) * C;
+#pragma unroll
+                            for (int q2 = 0; q2 < 4; ++q2)
+#pragma unroll
+                                for (int gp = 0; gp < 2; ++gp)
+                                    *reinterpret_cast<uint4*>(orow + 32 * q2 + 16 * gp + 8 * h) = opk[q2][gp];
+                        }
+#else
+                        if (win == 5) epi2_stage(0, opk);
+                        if (win == 6) { epi2_store(0, prev); epi2_stage(1, opk); }
+                        if (win == 7) epi2_store(1, prev);
+#endif
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
-        // ---- epilogue 1: relu(u) (bias is in the accumulator) -> bf16 B fragments; u > 0 bits
-        uint4 vf[4][2];
-        uint32_t mub[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t pk[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) pk[k] = relu2(pack2(acc[q][2 * k], acc[q][2 * k + 1]));
-            vf[q][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-            vf[q][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-            mub[q] = pos_bits16(pk);
-        }
-        // u > 0 bits by this layer's position: lane (r, h) -> words [h][0..3]
-        *reinterpret_cast<uint2*>(a.mu + ((size_t)b * a.T + p0 + c) * 8 + 4 * h) =
-            make_uint2(mub[0] | (mub[1] << 16), mub[2] | (mub[3] << 16));
+        STAMP(1)
 
-        // ---- GEMM 2 (1x1) + bias + residual ----
-        f32x16 acc2[4];
+        // ---- phase B: epilogue 1 (relu(u) -> bf16 B fragments, u > 0 bits) with GEMM 2 ----
 #pragma unroll
         for (int q2 = 0; q2 < 4; ++q2)
 #pragma unroll
@@ -280,43 +380,67 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
                 acc2[q2][4 * g + 0] = b4.x; acc2[q2][4 * g + 1] = b4.y;
                 acc2[q2][4 * g + 2] = b4.z; acc2[q2][4 * g + 3] = b4.w;
             }
+        uint4 vf[4][2];
+        uint32_t mub[4];
+        auto epi1 = [&](int q) {
+            uint32_t pk[8];
 #pragma unroll
-        for (int s = 0; s < 8; ++s)
+            for (int k = 0; k < 8; ++k) pk[k] = relu2(pack2(acc[q][2 * k], acc[q][2 * k + 1]));
+            vf[q][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            vf[q][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+            mub[q] = pos_bits16(pk);
+        };
+        {
+            // steps 0-7: W_r^T (A from LDS) x relu(u) (B in registers); steps 8-9: identity x e_l
+            // (residual; B = this wave's own rows); fragments fetched one step ahead
+            auto fetch = [&](int st, uint4 (&f)[4]) {
 #pragma unroll
-            for (int q2 = 0; q2 < 4; ++q2)
-                acc2[q2] = mfma_bf16(WRL[(q2 * 8 + s) * 64 + lane], vf[s >> 1][s & 1], acc2[q2]);
+                for (int q2 = 0; q2 < 4; ++q2)
+                    f[q2] = st < 8 ? WRL[(q2 * 8 + st) * 64 + lane]
+                                   : lds16(xb + RSB + (2 * q2 + (st - 8)) * 32);
+            };
+            uint4 fr[2][4];
+            fetch(0, fr[0]);
+            epi1(0);
 #pragma unroll
-        for (int q2 = 0; q2 < 4; ++q2)
+            for (int st = 0; st < 10; ++st) {
+                if (st + 1 < 10) fetch(st + 1, fr[(st + 1) & 1]);
+                if (st < 8) {
 #pragma unroll
-            for (int sg = 0; sg < 2; ++sg)
-                acc2[q2] = mfma_bf16(idf[sg], lds16(xb + RSB + (2 * q2 + sg) * 32), acc2[q2]);
-
-        // ---- epilogue 2: bf16 rows out (two 16-B pieces per lane pair), e_{l+1} > 0 bits ----
-        u16* orow = a.eout + ((size_t)b * a.T + tcol) * C;
-        uint32_t meb[4];
+                    for (int q2 = 0; q2 < 4; ++q2) acc2[q2] = mfma_bf16(fr[st & 1][q2], vf[st >> 1][st & 1], acc2[q2]);
+                } else {
 #pragma unroll
-        for (int q2 = 0; q2 < 4; ++q2) {
-            uint32_t o[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) o[k] = pack2(acc2[q2][2 * k], acc2[q2][2 * k + 1]);
-            meb[q2] = pos_bits16(o);
-#pragma unroll
-            for (int g = 0; g < 4; g += 2) {
-                // lanes h = 0 hold channels 8g..8g+3 (o[2g], o[2g+1]), h = 1 hold 8g+4..8g+7:
-                // swap so h = 0 holds group g whole and h = 1 group g+1 (guide T21)
-                uint32_t ax = o[2 * g], ay = o[2 * g + 1], bx = o[2 * g + 2], by = o[2 * g + 3];
-                auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
-                auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
-                ax = sx[0]; bx = sx[1]; ay = sy[0]; by = sy[1];
-                *reinterpret_cast<uint4*>(orow + 32 * q2 + 8 * g + 8 * h) = make_uint4(ax, ay, bx, by);
+                    for (int q2 = 0; q2 < 4; ++q2) acc2[q2] = mfma_bf16(idf[st - 8], fr[st & 1][q2], acc2[q2]);
+                }
+                if (st % 2 == 1 && st < 7) epi1((st + 1) / 2);
+                if (st == 7)   // u > 0 bits by this layer's position: lane (r, h) -> words [h][0..3]
+                    *reinterpret_cast<uint2*>(a.mu + ((size_t)cu.b * a.T + cu.p0 + c) * 8 + 4 * h) =
+                        make_uint2(mub[0] | (mub[1] << 16), mub[2] | (mub[3] << 16));
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
-        if (a.me_next) {
-            const int pn = (tcol & ((1 << a.dn_log2) - 1)) * a.nn + (tcol >> a.dn_log2);
-            *reinterpret_cast<uint2*>(a.me_next + ((size_t)b * a.T + pn) * 8 + 4 * h) =
-                make_uint2(meb[0] | (meb[1] << 16), meb[2] | (meb[3] << 16));
-        }
+        STAMP(2)
+        prev = cu;
+        ++it;
+    };
+
+    int tile = blockIdx.x;
+    if (tile < ntiles) {
+        body(std::integral_constant<bool, false>{}, tile);
+        for (tile += gridDim.x; tile < ntiles; tile += gridDim.x)
+            body(std::integral_constant<bool, true>{}, tile);
+        // drain: epilogue 2 of the last tile
+        uint4 opk[4][2];
+        uint32_t meb[4];
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) epi2_chunk(acc2[q2], opk[q2], meb[q2]);
+        me_store(prev, meb);
+        epi2_stage(0, opk);
+        epi2_store(0, prev);
+        epi2_stage(1, opk);
+        epi2_store(1, prev);
     }
+    STAMP_FLUSH(a.stamps)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 

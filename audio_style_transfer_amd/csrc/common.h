@@ -36,6 +36,25 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
+// Diagnostic phase stamps (guide: In-kernel stamps).  Only -DASTYLE_STAMPS builds execute
+// them; cycle deltas per phase are summed per wave and added to a.stamps[phase] at exit.
+#ifdef ASTYLE_STAMPS
+#define STAMP_DECL unsigned long long st_acc[12] = {}; unsigned long long st_prev = stamp_now();
+#define STAMP(k) { const unsigned long long st_t = stamp_now(); st_acc[k] += st_t - st_prev; st_prev = st_t; }
+#define STAMP_FLUSH(ptr) if (((threadIdx.x & 63) == 0) && (ptr)) { for (int k = 0; k < 12; ++k) atomicAdd(&(ptr)[k], st_acc[k]); }
+__device__ __forceinline__ unsigned long long stamp_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#else
+#define STAMP_DECL
+#define STAMP(k)
+#define STAMP_FLUSH(ptr)
+#endif
+
 // bf16 path (precision 1) tile geometry
 constexpr int TMB = 128;      // rows per encoder tile
 constexpr int XSB = 136;      // LDS row stride in bf16 (272 B: ds_read_b128 conflict-free)
@@ -56,6 +75,30 @@ __device__ __forceinline__ uint32_t relu2(uint32_t u) {         // bf16 relu == 
     v = __builtin_elementwise_max(v, (s16x2){0, 0});
     return __builtin_bit_cast(uint32_t, v);
 }
+// relu-mask word of one lane's 32x32 accumulator tile (bf16 path): bit mbit(i) = element i > 0
+// for the 16 elements held as 8 packed bf16 dwords (element 2k = low half of dword k).  The bit
+// order is the one pos_bits16 produces cheaply: 4 (i & 3) + (i >> 2).
+__host__ __device__ constexpr int mbit(int i) { return 4 * (i & 3) + (i >> 2); }
+__device__ __forceinline__ uint32_t pos_bits16(const uint32_t (&x)[8]) {
+    // x - 1 with int16 saturation has its sign bit clear iff x > 0 (bf16 -0 = 0x8000 saturates)
+    uint32_t t[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const s16x2 v = __builtin_elementwise_sub_sat(__builtin_bit_cast(s16x2, x[k]), (s16x2){1, 1});
+        t[k] = __builtin_bit_cast(uint32_t, v);
+    }
+    // bytes [t0.b1 t0.b3 t1.b1 t1.b3]: bit 7 of byte m = NOT(element 4j + m > 0)
+    uint32_t z = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t y = __builtin_amdgcn_perm(t[2 * j + 1], t[2 * j], 0x07050301u) & 0x80808080u;
+        z |= y >> (7 - j);                       // bit j of byte m
+    }
+    z ^= 0x0f0f0f0fu;                            // element 4j + m at bit 8m + j
+    const uint32_t u = z | (z >> 4);             // bytes 0, 2 hold nibbles (m = 0,1), (m = 2,3)
+    return __builtin_amdgcn_perm(u, u, 0x0c0c0200u);
+}
+
 __device__ __forceinline__ f32x16 mfma_bf16(uint4 a, uint4 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                     __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
@@ -104,6 +147,7 @@ struct BwdArgsB {
 
 // column-owning bf16 block forward (block_fwd_bf16.hip)
 struct FwdArgsC {
+    unsigned long long* stamps;            // diagnostic builds (-DASTYLE_STAMPS) only
     const u16* ein; u16* eout;
     const u16* wf;         // [3 taps][4 q][8 kb][64 lanes][8] W_d^T A fragments
     const u16* wrf;        // [4 q2][8 s][64][8] W_r^T A fragments, K in accumulator order

@@ -253,10 +253,12 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
         if (me0) {
             // e_0 > 0 bits for block 0's backward (dilation 1: position = time), in the MFMA
             // accumulator layout of block_fwd_bf16.hip: channels 4q..4q+3 = 32 Q + 8 g + 4 h + j
-            // with q = 8 Q + 2 g + h are bits 4g..4g+3 of word (h, Q)
-            uint32_t nib = ((short)(p0 & 0xffffu) > 0 ? 1u : 0u) | ((int)p0 >= 0x10000 ? 2u : 0u) |
-                           ((short)(p1 & 0xffffu) > 0 ? 4u : 0u) | ((int)p1 >= 0x10000 ? 8u : 0u);
-            nib <<= 4 * ((q >> 1) & 3);
+            // with q = 8 Q + 2 g + h are elements i = 4g + j of word (h, Q), at bits mbit(i)
+            const int g = (q >> 1) & 3;
+            uint32_t nib = (((short)(p0 & 0xffffu) > 0 ? 1u : 0u) << mbit(4 * g + 0)) |
+                           (((int)p0 >= 0x10000 ? 1u : 0u) << mbit(4 * g + 1)) |
+                           (((short)(p1 & 0xffffu) > 0 ? 1u : 0u) << mbit(4 * g + 2)) |
+                           (((int)p1 >= 0x10000 ? 1u : 0u) << mbit(4 * g + 3));
             nib |= (uint32_t)__shfl_xor((int)nib, 2);
             nib |= (uint32_t)__shfl_xor((int)nib, 4);
             if (((q >> 1) & 3) == 0) me0[rowi * 8 + (q & 1) * 4 + (q >> 3)] = (uint16_t)nib;

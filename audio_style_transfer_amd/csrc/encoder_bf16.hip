@@ -35,25 +35,6 @@ __device__ __forceinline__ uint4 relu8(uint4 v) {
 // accumulator register i of a 32x32 tile holds row (i&3) + 8(i>>2) + 4h (a channel here)
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-// Diagnostic phase stamps (guide: In-kernel stamps).  Only -DASTYLE_STAMPS builds execute
-// them; cycle deltas per phase are summed per wave and added to a.stamps[phase] at exit.
-#ifdef ASTYLE_STAMPS
-#define STAMP_DECL unsigned long long st_acc[12] = {}; unsigned long long st_prev = stamp_now();
-#define STAMP(k) { const unsigned long long st_t = stamp_now(); st_acc[k] += st_t - st_prev; st_prev = st_t; }
-#define STAMP_FLUSH(ptr) if (((threadIdx.x & 63) == 0) && (ptr)) { for (int k = 0; k < 12; ++k) atomicAdd(&(ptr)[k], st_acc[k]); }
-__device__ __forceinline__ unsigned long long stamp_now() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#else
-#define STAMP_DECL
-#define STAMP(k)
-#define STAMP_FLUSH(ptr)
-#endif
-
 struct Layout {            // uniform per launch
     int M;                 // segment length (positions); TMB when one segment (+ halos)
     int nrows;             // LDS rows of a tile
@@ -497,7 +478,7 @@ __global__ void __launch_bounds__(NTH, 1) k_block_bwd_bf16(BwdArgsB a, Layout ly
             const uint32_t mw = reinterpret_cast<const uint16_t*>(MU)[Lc[j] * 8 + h * 4 + (w & 3)];
             float v[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = ((mw >> i) & 1u) ? acc[j][i] : 0.f;
+            for (int i = 0; i < 16; ++i) v[i] = ((mw >> mbit(i)) & 1u) ? acc[j][i] : 0.f;
 #pragma unroll
             for (int g = 0; g < 4; ++g)
                 *reinterpret_cast<uint2*>(&U[Lc[j] * XSB + cb + 8 * g + 4 * h]) =
@@ -519,7 +500,7 @@ __global__ void __launch_bounds__(NTH, 1) k_block_bwd_bf16(BwdArgsB a, Layout ly
                 const uint32_t mw = TT[hrow] >= 0 ? reinterpret_cast<const uint16_t*>(MU)[hrow * 8 + h * 4 + (w & 3)] : 0u;
                 float v[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] = ((mw >> i) & 1u) ? hacc[i] : 0.f;
+                for (int i = 0; i < 16; ++i) v[i] = ((mw >> mbit(i)) & 1u) ? hacc[i] : 0.f;
 #pragma unroll
                 for (int g = 0; g < 4; ++g)
                     *reinterpret_cast<uint2*>(&U[hrow * XSB + cb + 8 * g + 4 * h]) =
@@ -570,11 +551,10 @@ __global__ void __launch_bounds__(NTH, 1) k_block_bwd_bf16(BwdArgsB a, Layout ly
             for (int g = 0; g < 4; ++g) {
                 uint2* pgp = reinterpret_cast<uint2*>(&G[Lc[j] * XSB + cb + 8 * g + 4 * h]);
                 const uint2 tv = *pgp;
-                const int Rr = 4 * g;   // element index of channel cb + 8 g + 4 h
-                const float o0 = bflo(tv.x) + (((mw >> (Rr + 0)) & 1u) ? acc[j][4 * g + 0] : 0.f);
-                const float o1 = bfhi(tv.x) + (((mw >> (Rr + 1)) & 1u) ? acc[j][4 * g + 1] : 0.f);
-                const float o2 = bflo(tv.y) + (((mw >> (Rr + 2)) & 1u) ? acc[j][4 * g + 2] : 0.f);
-                const float o3 = bfhi(tv.y) + (((mw >> (Rr + 3)) & 1u) ? acc[j][4 * g + 3] : 0.f);
+                const float o0 = bflo(tv.x) + (((mw >> mbit(4 * g + 0)) & 1u) ? acc[j][4 * g + 0] : 0.f);
+                const float o1 = bfhi(tv.x) + (((mw >> mbit(4 * g + 1)) & 1u) ? acc[j][4 * g + 1] : 0.f);
+                const float o2 = bflo(tv.y) + (((mw >> mbit(4 * g + 2)) & 1u) ? acc[j][4 * g + 2] : 0.f);
+                const float o3 = bfhi(tv.y) + (((mw >> mbit(4 * g + 3)) & 1u) ? acc[j][4 * g + 3] : 0.f);
                 *pgp = make_uint2(pack2(o0, o1), pack2(o2, o3));
             }
         }

@@ -2,7 +2,7 @@
 libastyle_stamps.so built with -DASTYLE_STAMPS).  Shares, not absolute time, are meaningful."""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ['ASTYLE_LIB'] = os.path.join(ROOT, 'audio_style_transfer_amd', 'libastyle_stamps.so')
+os.environ.setdefault('ASTYLE_LIB', os.path.join(ROOT, 'audio_style_transfer_amd', 'libastyle_stamps.so'))
 sys.path.insert(0, ROOT)
 import torch
 from audio_style_transfer_amd.engine import StyleEngine
@@ -18,8 +18,10 @@ lib.ast_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
 eng.forward(x); torch.cuda.synchronize()
 lib.ast_debug_stamps(None)
 v = buf.cpu().tolist()
-names = ['loop top', 'barrier A', 'commit', 'prefetch issue', 'barrier B', 'GEMM1', 'epilogue1',
-         'barrier C', 'mu store + GEMM2', 'epilogue2', 'barrier D', 'write-out']
+names = ['loop-top vmcnt wait', 'barrier', 'DMA issue', 'GEMM1', 'epilogue1 + mu', 'GEMM2',
+         'epilogue2 + stores', '-', '-', '-', '-', '-']
 tot = sum(v)
+tiles = B * 16384 // 128 * 30 / 256   # tiles per CU over the 30 block launches
 for n, c in zip(names, v):
-    print('%-18s %6.1f %%' % (n, 100.0 * c / tot))
+    if c:
+        print('%-20s %6.1f %%   %8.0f cycles/tile/wave' % (n, 100.0 * c / tot, c / (4 * 256 * tiles)))
