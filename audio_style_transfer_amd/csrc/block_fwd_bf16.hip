@@ -35,9 +35,15 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int FT = 256;                  // threads: one wave per SIMD
 constexpr int RSB = 272;                 // image row stride (bytes)
 constexpr int FROWS = TMB + 8;           // max image rows (4 segments of 32 + 2 pads each)
-constexpr int NDMA = (FROWS * RSB + 1023) / 1024;   // 37 one-KiB DMA groups per image
-constexpr int BUFB = NDMA * 1024;        // bytes per image (tail slack absorbs the last group)
-constexpr int DPW = (NDMA + 3) / 4;      // DMA groups per wave
+constexpr int NDMA = (FROWS * RSB + 1023) / 1024;   // 37 one-KiB groups per image
+constexpr int BUFB = NDMA * 1024;        // bytes per image
+// The DMA fills groups 0..35 (9 per wave, no per-wave tail branch); group 36 holds only the
+// last 128 B of row 135, which is a zero pad row of the 32-row segment layout (and unused by the
+// others): it is zeroed once at kernel start and never written again.
+constexpr int DPW = 9;
+static_assert(4 * DPW * 1024 >= 135 * RSB + 128 && 4 * DPW * 1024 < FROWS * RSB,
+              "DMA groups must cover every image row but the tail of row 135");
+constexpr int SRB = 144;                 // staging row stride: one 128-B half row + 16 pad
 
 struct FLayout {           // uniform per launch (see pick_flayout)
     int M;                 // segment length; TMB = one segment with two halo rows
@@ -79,7 +85,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
     __shared__ __attribute__((aligned(16))) uint4 W1[4 * 8 * 64];  // W_d^T tap 1 A fragments
     __shared__ __attribute__((aligned(16))) uint4 WRL[4 * 8 * 64]; // W_r^T A fragments (K permuted)
     __shared__ __attribute__((aligned(16))) float BIAS[2 * C];     // b_d, b_r
-    __shared__ __attribute__((aligned(16))) uint8_t STG[4][16 * RSB]; // output staging, per wave
+    __shared__ __attribute__((aligned(16))) uint8_t STG[4][32 * SRB]; // output staging, per wave
 
     const int tiles = a.T / TMB;
     const int ntiles = a.B * tiles;
@@ -109,6 +115,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
         WRL[i] = *reinterpret_cast<const uint4*>(a.wrf + (size_t)i * 8);
     }
     if (tid < C) { BIAS[tid] = a.bd[tid]; BIAS[C + tid] = a.br[tid]; }
+    if (tid < 2 * 64)   // group 36 of both images (see DPW)
+        *reinterpret_cast<uint4*>(&XS[tid >> 6][4 * DPW * 1024 + (tid & 63) * 16]) = make_uint4(0, 0, 0, 0);
     // identity A fragments: element e of lane (r, h) is 1 iff r == 16 sg + 8 h + e
     uint4 idf[2];
 #pragma unroll
@@ -162,7 +170,6 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
         const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[buf][0] + (uint32_t)(w * 1024);
 #pragma unroll
         for (int j = 0; j < DPW; ++j) {
-            if (w + 4 * j >= NDMA) break;
             const u16* src = a.zero;
             if (MASKED) {
                 const int p = p0 + srow[j] - 1;
@@ -175,13 +182,11 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
         }
     };
 
-    // staged output rows: this lane's (round rho, piece k) row is wave column 16 rho + 4 k + lane/16
-    int otoff[2][4];
+    // staged output rows: piece k of a round is wave column 8 k + lane / 8
+    int otoff[4];
 #pragma unroll
-    for (int rho = 0; rho < 2; ++rho)
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            otoff[rho][k] = MASKED ? 0 : row_toff(frow(32 * w + 16 * rho + 4 * k + (lane >> 4), ly), ly, a.d);
+    for (int k = 0; k < 4; ++k)
+        otoff[k] = MASKED ? 0 : row_toff(frow(32 * w + 8 * k + (lane >> 3), ly), ly, a.d);
     uint8_t* stg = &STG[w][0];
 
     // ---- per-tile geometry ----------------------------------------------------------------
@@ -204,43 +209,51 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
     // ---- epilogue 2 pieces (run for the PREVIOUS tile while this tile's GEMM 1 runs) ------
     // chunk(q2): bf16 pack, e_{l+1} > 0 bits, half-wave swap (guide T21): afterwards lane (n, h)
     // holds 16-B chunks 4 q2 + 2 gp + h (gp = 0, 1) of row n
-    auto epi2_chunk = [&](const f32x16& acc2q, uint4 (&opk)[2], uint32_t& mebq) {
-        uint32_t o[8];
+    auto e2_pack = [&](const f32x16& acc2q, uint32_t (&o)[8]) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = pack2(acc2q[2 * k], acc2q[2 * k + 1]);
-        mebq = pos_bits16(o);
+    };
+    auto e2_swap = [&](const uint32_t (&o)[8], uint4 (&opk)[2]) {
 #pragma unroll
         for (int gp = 0; gp < 2; ++gp) {
             const int g = 2 * gp;
-            uint32_t ax = o[2 * g], ay = o[2 * g + 1], bx = o[2 * g + 2], by = o[2 * g + 3];
-            auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
-            auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+            auto sx = __builtin_amdgcn_permlane32_swap(o[2 * g], o[2 * g + 2], false, false);
+            auto sy = __builtin_amdgcn_permlane32_swap(o[2 * g + 1], o[2 * g + 3], false, false);
             opk[gp] = make_uint4(sx[0], sy[0], sx[1], sy[1]);
         }
     };
-    // round rho: rows 16 rho .. 16 rho + 15 of this wave go through the staging rows and leave
-    // as whole 256-B rows (16 lanes per row)
-    // The staging rows are written by half the lanes and read by all: a wave-scope fence keeps
-    // the compiler from hoisting one lane's read above another lane's write (or sinking a
-    // write above a read), which per-thread program order alone does not forbid.
+    auto epi2_chunk = [&](const f32x16& acc2q, uint4 (&opk)[2], uint32_t& mebq) {
+        uint32_t o[8];
+        e2_pack(acc2q, o);
+        mebq = pos_bits16(o);
+        e2_swap(o, opk);
+    };
+    // The staging rows are written and read by different lanes: a wave-scope fence keeps the
+    // compiler from hoisting one lane's read above another lane's write (or sinking a write
+    // above a read), which per-thread program order alone does not forbid.
     auto wave_fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
-    auto epi2_stage = [&](int rho, const uint4 (&opk)[4][2]) {
+    // round rho: channels 64 rho .. 64 rho + 63 (32-channel tiles 2 rho, 2 rho + 1) of the
+    // wave's 32 rows go through the staging rows and leave as whole 128-B lines (8 lanes per
+    // row half)
+    auto epi2_stage = [&](int rho, const uint4 (&opk)[2][2]) {
         wave_fence();
-        if ((r >> 4) == rho) {
 #pragma unroll
-            for (int q2 = 0; q2 < 4; ++q2)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int gp = 0; gp < 2; ++gp)
-                    *reinterpret_cast<uint4*>(stg + (r & 15) * RSB + (4 * q2 + 2 * gp + h) * 16) = opk[q2][gp];
-        }
+            for (int gp = 0; gp < 2; ++gp)
+                *reinterpret_cast<uint4*>(stg + r * SRB + (4 * j + 2 * gp + h) * 16) = opk[j][gp];
         wave_fence();
     };
     auto epi2_store = [&](int rho, const Tile& t) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint4 v = lds16(stg + (4 * k + (lane >> 4)) * RSB + (lane & 15) * 16);
-            const int tt = col_time(t, 32 * w + 16 * rho + 4 * k + (lane >> 4), otoff[rho][k]);
-            *reinterpret_cast<uint4*>(a.eout + ((size_t)t.b * a.T + tt) * C + (lane & 15) * 8) = v;
+            const uint4 v = lds16(stg + (8 * k + (lane >> 3)) * SRB + (lane & 7) * 16);
+            const int tt = col_time(t, 32 * w + 8 * k + (lane >> 3), otoff[k]);
+#ifndef ABL_NOSTORE
+            *reinterpret_cast<uint4*>(a.eout + ((size_t)t.b * a.T + tt) * C + 64 * rho + (lane & 7) * 8) = v;
+#else
+            if (v.x == 0x12345u && tt < 0) *reinterpret_cast<uint4*>(a.eout) = v;
+#endif
         }
     };
     auto me_store = [&](const Tile& t, const uint32_t (&meb)[4]) {
@@ -295,7 +308,6 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
         }
         const u16* nbase = a.ein + ((size_t)nx.b * a.T + nx.tb) * C;
         auto dma_slot = [&](int j) {
-            if (w + 4 * j >= NDMA) return;
             const u16* src = a.zero;
             if (MASKED) {
                 const int p = nx.p0 + srow[j] - 1;
@@ -316,8 +328,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
                 acc[q][4 * g + 0] = b4.x; acc[q][4 * g + 1] = b4.y;
                 acc[q][4 * g + 2] = b4.z; acc[q][4 * g + 3] = b4.w;
             }
-        uint4 opk[4][2];
+        uint4 opk[2][2];
         uint32_t meb[4];
+        uint32_t o2[8];
         {
             auto bload = [&](int st) { return lds16(xb + (st >> 3) * RSB + (st & 7) * 32); };
             uint4 bl[3], al[2][4];
@@ -343,28 +356,38 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) acc[q] = mfma_bf16(wr2[q][kb], bv, acc[q]);
                 }
-                // side work of window st / 3, placed in its last step
-                if (st % 3 == 2) {
-                    const int win = st / 3;
-                    if (win < 5) { dma_slot(2 * win); dma_slot(2 * win + 1); }
-                    if (PREV) {
-                        if (win < 4) epi2_chunk(acc2[win], opk[win], meb[win]);
-                        if (win == 4) me_store(prev, meb);
-#ifdef DBG_NOSTAGE
-                        if (win == 5) {
-                            u16* orow = a.eout + ((size_t)prev.b * a.T + col_time(prev, c, tcoff)) * C;
-#pragma unroll
-                            for (int q2 = 0; q2 < 4; ++q2)
-#pragma unroll
-                                for (int gp = 0; gp < 2; ++gp)
-                                    *reinterpret_cast<uint4*>(orow + 32 * q2 + 16 * gp + 8 * h) = opk[q2][gp];
-                        }
-#else
-                        if (win == 5) epi2_stage(0, opk);
-                        if (win == 6) { epi2_store(0, prev); epi2_stage(1, opk); }
-                        if (win == 7) epi2_store(1, prev);
+                // side work, spread so that every step carries a few independent instructions
+                // between its MFMAs: epilogue 2 of the previous tile (pack / mask bits / swap of
+                // 32-channel tile q2 in steps 3 q2 .. 3 q2 + 2, staging + whole-row stores in
+                // steps 15-22) and the next tile's DMA (steps 0-7, 16, 17, where the steps carry
+                // the fewest LDS reads).  The stores stay behind the last DMA (vmcnt(9) above).
+#ifndef ABL_NODMA
+                if (st < 4) { dma_slot(2 * st); dma_slot(2 * st + 1); }
+                if (st == 4) dma_slot(8);
 #endif
+#ifndef ABL_NOEPI2
+                if (PREV) {
+                    // tile q2 = 0, 1 in steps 0-5, staged at 6, stored at 10; q2 = 2, 3 in steps
+                    // 7-9 and 11-13, staged at 15, stored at 18
+                    constexpr int qs[24] = {0, 0, 0, 1, 1, 1, -1, 2, 2, 2, -1, 3, 3, 3, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+                    constexpr int ph[24] = {0, 1, 2, 0, 1, 2, -1, 0, 1, 2, -1, 0, 1, 2, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+                    if (qs[st] >= 0) {
+                        const int q2 = qs[st];
+                        if (ph[st] == 0) e2_pack(acc2[q2], o2);
+                        if (ph[st] == 1) meb[q2] = pos_bits16(o2);
+                        if (ph[st] == 2) e2_swap(o2, opk[q2 & 1]);
                     }
+                    if (st == 6) epi2_stage(0, opk);
+                    if (st == 10) epi2_store(0, prev);
+                    if (st == 14) me_store(prev, meb);
+                    if (st == 15) epi2_stage(1, opk);
+                    if (st == 18) epi2_store(1, prev);
+                }
+#endif
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // up to 4 VALU
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -382,40 +405,55 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
             }
         uint4 vf[4][2];
         uint32_t mub[4];
-        auto epi1 = [&](int q) {
+        auto epi1a = [&](int q) {      // relu(u) -> bf16 B fragments (bias is in the accumulator)
             uint32_t pk[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) pk[k] = relu2(pack2(acc[q][2 * k], acc[q][2 * k + 1]));
             vf[q][0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
             vf[q][1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+        };
+        auto epi1b = [&](int q) {      // u > 0 bits
+            const uint32_t pk[8] = {vf[q][0].x, vf[q][0].y, vf[q][0].z, vf[q][0].w,
+                                    vf[q][1].x, vf[q][1].y, vf[q][1].z, vf[q][1].w};
             mub[q] = pos_bits16(pk);
         };
         {
-            // steps 0-7: W_r^T (A from LDS) x relu(u) (B in registers); steps 8-9: identity x e_l
-            // (residual; B = this wave's own rows); fragments fetched one step ahead
+            // steps 0-1: identity x e_l (the residual; B = this wave's own rows), steps 2-9:
+            // W_r^T (A from LDS) x relu(u) (B in registers); fragments fetched one step ahead.
+            // Epilogue 1 of tile q runs under the two steps before the first one that needs it.
             auto fetch = [&](int st, uint4 (&f)[4]) {
 #pragma unroll
                 for (int q2 = 0; q2 < 4; ++q2)
-                    f[q2] = st < 8 ? WRL[(q2 * 8 + st) * 64 + lane]
-                                   : lds16(xb + RSB + (2 * q2 + (st - 8)) * 32);
+                    f[q2] = st >= 2 ? WRL[(q2 * 8 + (st - 2)) * 64 + lane]
+                                    : lds16(xb + RSB + (2 * q2 + st) * 32);
             };
             uint4 fr[2][4];
             fetch(0, fr[0]);
-            epi1(0);
 #pragma unroll
             for (int st = 0; st < 10; ++st) {
                 if (st + 1 < 10) fetch(st + 1, fr[(st + 1) & 1]);
-                if (st < 8) {
+                if (st < 2) {
 #pragma unroll
-                    for (int q2 = 0; q2 < 4; ++q2) acc2[q2] = mfma_bf16(fr[st & 1][q2], vf[st >> 1][st & 1], acc2[q2]);
+                    for (int q2 = 0; q2 < 4; ++q2) acc2[q2] = mfma_bf16(idf[st], fr[st & 1][q2], acc2[q2]);
                 } else {
+                    const int k = st - 2;
 #pragma unroll
-                    for (int q2 = 0; q2 < 4; ++q2) acc2[q2] = mfma_bf16(idf[st - 8], fr[st & 1][q2], acc2[q2]);
+                    for (int q2 = 0; q2 < 4; ++q2) acc2[q2] = mfma_bf16(fr[st & 1][q2], vf[k >> 1][k & 1], acc2[q2]);
                 }
-                if (st % 2 == 1 && st < 7) epi1((st + 1) / 2);
-                if (st == 7)   // u > 0 bits by this layer's position: lane (r, h) -> words [h][0..3]
+                // epilogue 1 of tile q: part a at step 2q - 2, part b at step 2q - 1 (q = 0
+                // under the identity steps); the mask store after the last one
+                if (st < 8) {
+                    const int q = st / 2;
+                    if (st % 2 == 0) epi1a(q); else epi1b(q);
+                }
+                if (st == 8)   // u > 0 bits by this layer's position: lane (r, h) -> words [h][0..3]
                     *reinterpret_cast<uint2*>(a.mu + ((size_t)cu.b * a.T + cu.p0 + c) * 8 + 4 * h) =
                         make_uint2(mub[0] | (mub[1] << 16), mub[2] | (mub[3] << 16));
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -430,15 +468,16 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
         for (tile += gridDim.x; tile < ntiles; tile += gridDim.x)
             body(std::integral_constant<bool, true>{}, tile);
         // drain: epilogue 2 of the last tile
-        uint4 opk[4][2];
+        uint4 opk[2][2];
         uint32_t meb[4];
 #pragma unroll
-        for (int q2 = 0; q2 < 4; ++q2) epi2_chunk(acc2[q2], opk[q2], meb[q2]);
+        for (int rho = 0; rho < 2; ++rho) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) epi2_chunk(acc2[2 * rho + j], opk[j], meb[2 * rho + j]);
+            epi2_stage(rho, opk);
+            epi2_store(rho, prev);
+        }
         me_store(prev, meb);
-        epi2_stage(0, opk);
-        epi2_store(0, prev);
-        epi2_stage(1, opk);
-        epi2_store(1, prev);
     }
     STAMP_FLUSH(a.stamps)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
