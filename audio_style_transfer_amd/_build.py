@@ -10,13 +10,15 @@ from concurrent.futures import ThreadPoolExecutor
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, 'csrc')
 LIB = os.path.join(PKG, 'libastyle.so')
-SOURCES = ['encoder.hip', 'encoder_bf16.hip', 'block_fwd_bf16.hip', 'gram.hip', 'gram_bf16.hip', 'gram_gatys.hip', 'api.hip']
+SOURCES = ['encoder.hip', 'encoder_bf16.hip', 'block_fwd_bf16.hip', 'block_bwd_bf16.hip', 'gram.hip',
+           'gram_bf16.hip', 'gram_gatys.hip', 'api.hip']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall',
          '-Wno-unused-function', '-munsafe-fp-atomics']
 # per-source extras: the column-owning block kernels keep their weights in AGPRs (asm-loaded)
 # and need the MFMA accumulators in arch VGPRs, where the epilogues read them without copies
-EXTRA = {'block_fwd_bf16.hip': ['-mllvm', '-amdgpu-mfma-vgpr-form=1']}
+EXTRA = {'block_fwd_bf16.hip': ['-mllvm', '-amdgpu-mfma-vgpr-form=1'],
+         'block_bwd_bf16.hip': ['-mllvm', '-amdgpu-mfma-vgpr-form=1']}
 
 
 def _stale() -> bool:

@@ -48,8 +48,11 @@ constexpr size_t W_TOTAL = BB_OFF + 16;
 constexpr size_t WDB = 0, WDTB = 3 * C * C, WRB = 6 * C * C, WRTB = 7 * C * C;
 // MFMA A-fragment order for block_fwd_bf16.hip: WFB [3 taps][4 q][8 kb][64 lanes][8],
 // lane (m, h) element e = W_d[tap][ci = 16 kb + 8 h + e][co = 32 q + m];
-// WRFB [4 q2][8 s][64][8], element e = W_r[co = kperm(s, h, e)][co2 = 32 q2 + m]
-constexpr size_t WFB = 8 * C * C, WRFB = 11 * C * C, BLKB_SZ = 12 * C * C;
+// WRFB [4 q2][8 s][64][8], element e = W_r[co = kperm(s, h, e)][co2 = 32 q2 + m].
+// block_bwd_bf16.hip: WBFB [3][4 q][8 kb][64][8], element e = W_d[tap][32 q + m][16 kb + 8 h + e];
+// WRBFB [4 q][8 kb][64][8], element e = W_r[32 q + m][16 kb + 8 h + e]
+constexpr size_t WFB = 8 * C * C, WRFB = 11 * C * C, WBFB = 12 * C * C, WRBFB = 15 * C * C,
+                 BLKB_SZ = 16 * C * C;
 inline int kperm(int s, int h, int e) { return 32 * (s >> 1) + 16 * (s & 1) + (e & 3) + 8 * (e >> 2) + 4 * h; }
 
 uint16_t host_bf16(float f) {   // round to nearest even
@@ -404,19 +407,23 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                         tr[(size_t)k * C * C + co * C + ci] = host[(size_t)k * C * C + ci * C + co];
             if ((rc = put(base + WD, host, 3 * C * C))) return rc;
             if ((rc = put(base + WDT, tr.data(), 3 * C * C))) return rc;
-            std::vector<uint16_t> hb(6 * C * C), hf(3 * C * C);
+            std::vector<uint16_t> hb(6 * C * C), hf(3 * C * C), hg(3 * C * C);
             for (size_t i = 0; i < 3 * C * C; ++i) { hb[i] = host_bf16(host[i]); hb[3 * C * C + i] = host_bf16(tr[i]); }
+            // forward fragments from W_d, backward fragments the same order from W_d^T
             for (int k = 0; k < 3; ++k)
                 for (int q = 0; q < 4; ++q)
                     for (int kb = 0; kb < 8; ++kb)
                         for (int ln = 0; ln < 64; ++ln)
                             for (int e = 0; e < 8; ++e) {
                                 const int ci = 16 * kb + 8 * (ln >> 5) + e, co = 32 * q + (ln & 31);
-                                hf[((((size_t)k * 4 + q) * 8 + kb) * 64 + ln) * 8 + e] = hb[(size_t)k * C * C + ci * C + co];
+                                const size_t o = ((((size_t)k * 4 + q) * 8 + kb) * 64 + ln) * 8 + e;
+                                hf[o] = hb[(size_t)k * C * C + ci * C + co];
+                                hg[o] = hb[3 * C * C + (size_t)k * C * C + ci * C + co];
                             }
             u16* dst = x->wtsb + (size_t)(l - 1) * BLKB_SZ;
             HIPCHK(hipMemcpy(dst + WDB, hb.data(), 6 * C * C * 2, hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(dst + WFB, hf.data(), 3 * C * C * 2, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(dst + WBFB, hg.data(), 3 * C * C * 2, hipMemcpyHostToDevice));
             return 0;
         }
         if (!strcmp(tail, "biases")) { if ((rc = need(C))) return rc; return put(base + BD, host, C); }
@@ -430,18 +437,22 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                 for (int co = 0; co < C; ++co) tr[co * C + ci] = host[ci * C + co];
             if ((rc = put(base + WR, host, C * C))) return rc;
             if ((rc = put(base + WRT, tr.data(), C * C))) return rc;
-            std::vector<uint16_t> hb(2 * C * C), hf(C * C);
+            std::vector<uint16_t> hb(2 * C * C), hf(C * C), hg(C * C);
             for (size_t i = 0; i < C * C; ++i) { hb[i] = host_bf16(host[i]); hb[C * C + i] = host_bf16(tr[i]); }
             for (int q2 = 0; q2 < 4; ++q2)
                 for (int st = 0; st < 8; ++st)
                     for (int ln = 0; ln < 64; ++ln)
                         for (int e = 0; e < 8; ++e) {
                             const int co = kperm(st, ln >> 5, e), co2 = 32 * q2 + (ln & 31);
-                            hf[(((size_t)q2 * 8 + st) * 64 + ln) * 8 + e] = hb[(size_t)co * C + co2];
+                            const size_t o = (((size_t)q2 * 8 + st) * 64 + ln) * 8 + e;
+                            hf[o] = hb[(size_t)co * C + co2];
+                            // backward: W_r[32 q + m][16 kb + 8 h + e] = W_r^T[16 kb + 8 h + e][32 q + m]
+                            hg[o] = hb[C * C + (size_t)(16 * st + 8 * (ln >> 5) + e) * C + 32 * q2 + (ln & 31)];
                         }
             u16* dst = x->wtsb + (size_t)(l - 1) * BLKB_SZ;
             HIPCHK(hipMemcpy(dst + WRB, hb.data(), 2 * C * C * 2, hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(dst + WRFB, hf.data(), C * C * 2, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(dst + WRBFB, hg.data(), C * C * 2, hipMemcpyHostToDevice));
             return 0;
         }
         if (!strcmp(tail, "biases")) { if ((rc = need(C))) return rc; return put(base + BR, host, C); }
@@ -583,23 +594,31 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     }
     tmark(x, s);
     // backward chain through the blocks
+    auto direct = [&](int t) -> const void* {   // D_t: direct loss gradient of tensor t (or null)
+        return x->tensor_in_style[t] ? tens(x, t) : x->cg_buf[t];
+    };
     for (int l = x->nblk - 1; l >= 0; --l) {
         float* w = blkw(x, l);
         const int tin = l + 1;
         const void* gin = (l == x->nblk - 1) ? nullptr : x->chain[(l + 1) & 1];
-        const void* din = x->tensor_in_style[tin] ? tens(x, tin) : x->cg_buf[tin];
+        const void* din = direct(tin);
         const uint32_t* mu = x->mu + (size_t)l * c.batch * c.T * 4;
         const uint32_t* me = x->me + (size_t)l * c.batch * c.T * 4;
         const int d = 1 << (l % 10);
         if (x->bf) {
-            BwdArgsB a;
+            // the bf16 chain holds d loss / d e_l with D_l already added (the kernel adds it)
+            BwdArgsC a;
             a.stamps = g_stamps;
             u16* wb = blkwb(x, l);
-            a.gin = (const u16*)gin; a.din = (const u16*)din; a.gout = (u16*)x->chain[l & 1];
-            a.wr = wb + WRB; a.wr32 = w + WR; a.wd = wb + WDB;
-            a.mu = mu; a.me = me;
+            a.tin = (const u16*)(gin ? gin : din);
+            a.dadd = l > 0 ? (const u16*)direct(l) : nullptr;
+            a.gout = (u16*)x->chain[l & 1];
+            a.wbf = wb + WBFB; a.wrb = wb + WRBFB;
+            a.mu = (const uint16_t*)mu; a.me = (const uint16_t*)me;
+            a.zero = (const u16*)x->zero;
             a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
-            launch_block_bwd_bf16(a, s);
+            if (!a.tin) return fail(AST_E_STATE, "top block has no loss gradient");
+            launch_block_bwd_c(a, s);
         } else {
             BwdArgs a;
             a.gin = (const float*)gin; a.din = (const float*)din; a.gout = (float*)x->chain[l & 1];

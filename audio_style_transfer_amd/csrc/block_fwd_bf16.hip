@@ -23,64 +23,16 @@
 //    lane's 32x32 tile, common.h): u > 0 by this layer's position, e_{l+1} > 0 by the NEXT layer's
 //    position, so the backward applies them with no bit shuffling (block_bwd in
 //    encoder_bf16.hip).
-#include "common.h"
+#include "colwave.h"
 #include <algorithm>
 #include <type_traits>
 
 namespace ast {
 namespace {
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int FT = 256;                  // threads: one wave per SIMD
-constexpr int RSB = 272;                 // image row stride (bytes)
-constexpr int FROWS = TMB + 8;           // max image rows (4 segments of 32 + 2 pads each)
-constexpr int NDMA = (FROWS * RSB + 1023) / 1024;   // 37 one-KiB groups per image
-constexpr int BUFB = NDMA * 1024;        // bytes per image
-// The DMA fills groups 0..35 (9 per wave, no per-wave tail branch); group 36 holds only the
-// last 128 B of row 135, which is a zero pad row of the 32-row segment layout (and unused by the
-// others): it is zeroed once at kernel start and never written again.
-constexpr int DPW = 9;
-static_assert(4 * DPW * 1024 >= 135 * RSB + 128 && 4 * DPW * 1024 < FROWS * RSB,
-              "DMA groups must cover every image row but the tail of row 135");
-constexpr int SRB = 144;                 // staging row stride: one 128-B half row + 16 pad
-
-struct FLayout {           // uniform per launch (see pick_flayout)
-    int M;                 // segment length; TMB = one segment with two halo rows
-    int nrows;             // image rows
-};
-
-__device__ __forceinline__ int frow(int c, const FLayout& ly) {   // image row of column c
-    return (c / ly.M) * (ly.M + 2) + 1 + (c % ly.M);
-}
-
-// time offset of image row L from the tile's base time (unmasked layouts):
-//   one segment: rows are positions p0-1 .. p0+128 of one sub-sequence, t = tb + (L-1) d
-//   segments of M = n: row (s, k) is position k-1 of sub-sequence j0 + s, t = tb + (k-1) d + s
-__device__ __forceinline__ int row_toff(int L, const FLayout& ly, int d) {
-    if (ly.M == TMB) return (L - 1) * d;
-    const int s = L / (ly.M + 2), k = L - s * (ly.M + 2);
-    return (k - 1) * d + s;
-}
-
-__device__ __forceinline__ uint4 relu8(uint4 v) {
-    return make_uint4(relu2(v.x), relu2(v.y), relu2(v.z), relu2(v.w));
-}
-
-__device__ __forceinline__ uint4 lds16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
-
-// 16 B per lane HBM -> LDS at lds_base + 16 * lane (global_load_lds_dwordx4).  Inline asm so the
-// compiler neither counts it nor drains it with vmcnt(0) before unrelated LDS reads: the kernel
-// waits for it explicitly (cdna_hip_programming.md §5.7).
-__device__ __forceinline__ void dma16(const void* src, uint32_t lds_base) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(lds_base) : "memory");
-}
+using namespace cw;
 
 template <bool MASKED>
-__global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
+__global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, Layout ly) {
     __shared__ __attribute__((aligned(16))) uint8_t XS[2][BUFB];   // e_l tile images
     __shared__ __attribute__((aligned(16))) uint4 W1[4 * 8 * 64];  // W_d^T tap 1 A fragments
     __shared__ __attribute__((aligned(16))) uint4 WRL[4 * 8 * 64]; // W_r^T A fragments (K permuted)
@@ -102,13 +54,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
     for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int kb = 0; kb < 8; ++kb) {
-            const uint4 v0 = *reinterpret_cast<const uint4*>(a.wf + ((size_t)((0 * 4 + q) * 8 + kb) * 64 + lane) * 8);
-            const uint4 v2 = *reinterpret_cast<const uint4*>(a.wf + ((size_t)((2 * 4 + q) * 8 + kb) * 64 + lane) * 8);
-            u32x4 t0 = __builtin_bit_cast(u32x4, v0), t2 = __builtin_bit_cast(u32x4, v2);
-            asm volatile("" : "=a"(t0) : "0"(t0));
-            asm volatile("" : "=a"(t2) : "0"(t2));
-            wr0[q][kb] = __builtin_bit_cast(uint4, t0);
-            wr2[q][kb] = __builtin_bit_cast(uint4, t2);
+            wr0[q][kb] = to_agpr(*reinterpret_cast<const uint4*>(a.wf + ((size_t)((0 * 4 + q) * 8 + kb) * 64 + lane) * 8));
+            wr2[q][kb] = to_agpr(*reinterpret_cast<const uint4*>(a.wf + ((size_t)((2 * 4 + q) * 8 + kb) * 64 + lane) * 8));
         }
     for (int i = tid; i < 4 * 8 * 64; i += FT) {
         W1[i] = *reinterpret_cast<const uint4*>(a.wf + ((size_t)4 * 8 * 64 + i) * 8);
@@ -117,70 +64,14 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
     if (tid < C) { BIAS[tid] = a.bd[tid]; BIAS[C + tid] = a.br[tid]; }
     if (tid < 2 * 64)   // group 36 of both images (see DPW)
         *reinterpret_cast<uint4*>(&XS[tid >> 6][4 * DPW * 1024 + (tid & 63) * 16]) = make_uint4(0, 0, 0, 0);
-    // identity A fragments: element e of lane (r, h) is 1 iff r == 16 sg + 8 h + e
-    uint4 idf[2];
-#pragma unroll
-    for (int sg = 0; sg < 2; ++sg) {
-        const int e = r - 16 * sg - 8 * h;
-        uint32_t dw[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            dw[k] = (e == 2 * k ? 0x3f80u : 0u) | (e == 2 * k + 1 ? 0x3f800000u : 0u);
-        idf[sg] = make_uint4(dw[0], dw[1], dw[2], dw[3]);
-    }
+    const uint4 idf[2] = {identity_frag(0, r, h), identity_frag(1, r, h)};
 
     const int c = 32 * w + r;                  // this lane's tile column
     const int Lc = frow(c, ly);
     const int tcoff = MASKED ? 0 : row_toff(Lc, ly, a.d);
-
-    // DMA slots: group g = w + 4 j covers image bytes [1024 g, 1024 g + 1024); this lane's
-    // 16 B land at row L, chunk qc (qc == 16: the pad slot, filled from chunk 0)
-    int soff[DPW];       // source element offset from the tile's base row (unmasked layouts)
-    int scls[DPW];       // source class: 0 row, 1 zero, 2 left halo, 3 right halo
-    int srow[DPW], schk[DPW];
-#pragma unroll
-    for (int j = 0; j < DPW; ++j) {
-        const int g = w + 4 * j;
-        const int o = g * 1024 + lane * 16;
-        const int L = o / RSB, qc = (o - L * RSB) >> 4;
-        const int ch = qc < 16 ? qc : 0;
-        srow[j] = L;
-        schk[j] = ch;
-        int cls = 0;
-        if (L >= ly.nrows) cls = 1;
-        else if (ly.M == TMB) cls = L == 0 ? 2 : (L == TMB + 1 ? 3 : 0);
-        else {
-            const int k = L % (ly.M + 2);
-            cls = (k == 0 || k == ly.M + 1) ? 1 : 0;
-        }
-        scls[j] = cls;
-        soff[j] = MASKED || cls == 1 ? 0 : row_toff(L, ly, a.d) * C + ch * 8;
-    }
+    ImageDma<MASKED> dma;
+    dma.init(w, lane, ly, a.d);
     __syncthreads();
-
-    auto stage = [&](int tl, int buf) {          // DMA of a whole tile image (prologue)
-        const int b = tl / tiles, p0 = (tl - b * tiles) * TMB;
-        int m0 = 0, tb = 0;
-        if (!MASKED) {
-            if (ly.M == TMB) { m0 = p0 % a.n; tb = m0 * a.d + p0 / a.n; }
-            else tb = p0 / a.n;
-        }
-        const uint32_t vmask = 1u | (!MASKED && ly.M == TMB && m0 > 0 ? 4u : 0u) |
-                               (!MASKED && ly.M == TMB && m0 + TMB < a.n ? 8u : 0u);
-        const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[buf][0] + (uint32_t)(w * 1024);
-#pragma unroll
-        for (int j = 0; j < DPW; ++j) {
-            const u16* src = a.zero;
-            if (MASKED) {
-                const int p = p0 + srow[j] - 1;
-                if (scls[j] != 1 && p >= 0 && p < a.T)
-                    src = a.ein + ((size_t)b * a.T + (p % a.n) * a.d + p / a.n) * C + schk[j] * 8;
-            } else if ((vmask >> scls[j]) & 1u) {
-                src = a.ein + ((size_t)b * a.T + tb) * C + soff[j];
-            }
-            dma16(src, lds0 + j * 4096);
-        }
-    };
 
     // staged output rows: piece k of a round is wave column 8 k + lane / 8
     int otoff[4];
@@ -189,49 +80,18 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
         otoff[k] = MASKED ? 0 : row_toff(frow(32 * w + 8 * k + (lane >> 3), ly), ly, a.d);
     uint8_t* stg = &STG[w][0];
 
-    // ---- per-tile geometry ----------------------------------------------------------------
-    struct Tile { int b, p0, tb; };
-    auto tile_at = [&](int tl) {
-        Tile t;
-        t.b = tl / tiles;
-        t.p0 = (tl - t.b * tiles) * TMB;
-        t.tb = MASKED ? 0 : (ly.M == TMB ? (t.p0 % a.n) * a.d + t.p0 / a.n : t.p0 / a.n);
-        return t;
-    };
-    auto col_time = [&](const Tile& t, int cc, int toff) {   // time of tile column cc
-        if (MASKED) {
-            const int p = t.p0 + cc;
-            return (p % a.n) * a.d + p / a.n;
-        }
-        return t.tb + toff;
-    };
+    auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, tiles, a.n, a.d, ly); };
+    auto ctime = [&](const Tile& t, int cc, int toff) { return col_time<MASKED>(t, cc, toff, a.n, a.d); };
 
     // ---- epilogue 2 pieces (run for the PREVIOUS tile while this tile's GEMM 1 runs) ------
-    // chunk(q2): bf16 pack, e_{l+1} > 0 bits, half-wave swap (guide T21): afterwards lane (n, h)
-    // holds 16-B chunks 4 q2 + 2 gp + h (gp = 0, 1) of row n
-    auto e2_pack = [&](const f32x16& acc2q, uint32_t (&o)[8]) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = pack2(acc2q[2 * k], acc2q[2 * k + 1]);
-    };
-    auto e2_swap = [&](const uint32_t (&o)[8], uint4 (&opk)[2]) {
-#pragma unroll
-        for (int gp = 0; gp < 2; ++gp) {
-            const int g = 2 * gp;
-            auto sx = __builtin_amdgcn_permlane32_swap(o[2 * g], o[2 * g + 2], false, false);
-            auto sy = __builtin_amdgcn_permlane32_swap(o[2 * g + 1], o[2 * g + 3], false, false);
-            opk[gp] = make_uint4(sx[0], sy[0], sx[1], sy[1]);
-        }
-    };
+    // chunk(q2): bf16 pack, e_{l+1} > 0 bits, half-wave swap: afterwards lane (n, h) holds
+    // 16-B chunks 4 q2 + 2 gp + h (gp = 0, 1) of row n
     auto epi2_chunk = [&](const f32x16& acc2q, uint4 (&opk)[2], uint32_t& mebq) {
         uint32_t o[8];
-        e2_pack(acc2q, o);
+        pack_tile(acc2q, o);
         mebq = pos_bits16(o);
-        e2_swap(o, opk);
+        swap_tile(o, opk);
     };
-    // The staging rows are written and read by different lanes: a wave-scope fence keeps the
-    // compiler from hoisting one lane's read above another lane's write (or sinking a write
-    // above a read), which per-thread program order alone does not forbid.
-    auto wave_fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
     // round rho: channels 64 rho .. 64 rho + 63 (32-channel tiles 2 rho, 2 rho + 1) of the
     // wave's 32 rows go through the staging rows and leave as whole 128-B lines (8 lanes per
     // row half)
@@ -248,7 +108,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint4 v = lds16(stg + (8 * k + (lane >> 3)) * SRB + (lane & 7) * 16);
-            const int tt = col_time(t, 32 * w + 8 * k + (lane >> 3), otoff[k]);
+            const int tt = ctime(t, 32 * w + 8 * k + (lane >> 3), otoff[k]);
 #ifndef ABL_NOSTORE
             *reinterpret_cast<uint4*>(a.eout + ((size_t)t.b * a.T + tt) * C + 64 * rho + (lane & 7) * 8) = v;
 #else
@@ -258,15 +118,20 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
     };
     auto me_store = [&](const Tile& t, const uint32_t (&meb)[4]) {
         if (a.me_next) {
-            const int tc = col_time(t, c, tcoff);
+            const int tc = ctime(t, c, tcoff);
             const int pn = (tc & ((1 << a.dn_log2) - 1)) * a.nn + (tc >> a.dn_log2);
             *reinterpret_cast<uint2*>(a.me_next + ((size_t)t.b * a.T + pn) * 8 + 4 * h) =
                 make_uint2(meb[0] | (meb[1] << 16), meb[2] | (meb[3] << 16));
         }
     };
 
-    stage(blockIdx.x, 0);
-    f32x16 acc[4];                  // GEMM 1 accumulators
+    if (blockIdx.x < ntiles) {                  // prologue: the first tile's image
+        dma.aim(a.ein, tile_of(blockIdx.x), ly, a.T, a.n);
+        const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[0][0] + (uint32_t)(w * 1024);
+#pragma unroll
+        for (int j = 0; j < DPW; ++j) dma.issue(j, a.ein, a.zero, lds0, a.T, a.n, a.d);
+    }
+    f32x16 acc[4];                 // GEMM 1 accumulators
     f32x16 acc2[4];                 // GEMM 2 accumulators, carried into the next iteration
     Tile prev{0, 0, 0};
     int it = 0;
@@ -279,7 +144,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
     auto body = [&](auto has_prev, int tile) {
         constexpr bool PREV = decltype(has_prev)::value;
         const int cur = it & 1;
-        const Tile cu = tile_at(tile);
+        const Tile cu = tile_of(tile);
         // this wave's DMA of the current image is complete (only the <= 10 stores of the
         // previous tile, issued after it, may still be in flight: vmcnt counts in issue order);
         // the barrier publishes every wave's part and retires all reads of the other image
@@ -299,25 +164,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
 
         // next tile's DMA: source pointers of the wave's slots
         const int ntl = tile + gridDim.x < ntiles ? tile + gridDim.x : ntiles - 1;
-        const Tile nx = tile_at(ntl);
         const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[cur ^ 1][0] + (uint32_t)(w * 1024);
-        uint32_t vmask = 1u;
-        if (!MASKED && ly.M == TMB) {
-            const int m0 = nx.p0 % a.n;
-            vmask |= (m0 > 0 ? 4u : 0u) | (m0 + TMB < a.n ? 8u : 0u);
-        }
-        const u16* nbase = a.ein + ((size_t)nx.b * a.T + nx.tb) * C;
-        auto dma_slot = [&](int j) {
-            const u16* src = a.zero;
-            if (MASKED) {
-                const int p = nx.p0 + srow[j] - 1;
-                if (scls[j] != 1 && p >= 0 && p < a.T)
-                    src = a.ein + ((size_t)nx.b * a.T + (p % a.n) * a.d + p / a.n) * C + schk[j] * 8;
-            } else if ((vmask >> scls[j]) & 1u) {
-                src = nbase + soff[j];
-            }
-            dma16(src, lds0 + j * 4096);
-        };
+        dma.aim(a.ein, tile_of(ntl), ly, a.T, a.n);
+        auto dma_slot = [&](int j) { dma.issue(j, a.ein, a.zero, lds0, a.T, a.n, a.d); };
 
         // ---- phase A ----
 #pragma unroll
@@ -373,9 +222,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
                     constexpr int ph[24] = {0, 1, 2, 0, 1, 2, -1, 0, 1, 2, -1, 0, 1, 2, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
                     if (qs[st] >= 0) {
                         const int q2 = qs[st];
-                        if (ph[st] == 0) e2_pack(acc2[q2], o2);
+                        if (ph[st] == 0) pack_tile(acc2[q2], o2);
                         if (ph[st] == 1) meb[q2] = pos_bits16(o2);
-                        if (ph[st] == 2) e2_swap(o2, opk[q2 & 1]);
+                        if (ph[st] == 2) swap_tile(o2, opk[q2 & 1]);
                     }
                     if (st == 6) epi2_stage(0, opk);
                     if (st == 10) epi2_store(0, prev);
@@ -483,33 +332,25 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, FLayout ly) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-int g_cus_c = 0;
-int num_cus_c() {
-    if (!g_cus_c) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&g_cus_c, hipDeviceAttributeMultiprocessorCount, dev);
-        if (g_cus_c <= 0) g_cus_c = 256;
-    }
-    return g_cus_c;
-}
-
-// Segment layout when a tile lies inside one sub-sequence (n % 128 == 0) or holds whole
-// sub-sequences of >= 32 positions; otherwise one segment with per-column tap masks.
-bool pick_flayout(int n, FLayout& ly) {
-    if (n % TMB == 0) { ly.M = TMB; ly.nrows = TMB + 2; return false; }
-    if (n < TMB && TMB % n == 0 && n >= 32) { ly.M = n; ly.nrows = (TMB / n) * (n + 2); return false; }
-    ly.M = TMB; ly.nrows = TMB + 2;
-    return true;
-}
+int g_cus = 0;
 
 }  // namespace
 
+int cw::num_cus() {
+    if (!g_cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_cus <= 0) g_cus = 256;
+    }
+    return g_cus;
+}
+
 void launch_block_fwd_c(const FwdArgsC& a, hipStream_t s) {
     const int nt = a.B * (a.T / TMB);
-    const dim3 grid(std::min(nt, num_cus_c()));
-    FLayout ly;
-    if (pick_flayout(a.n, ly)) hipLaunchKernelGGL(k_block_fwd_c<true>, grid, dim3(FT), 0, s, a, ly);
+    const dim3 grid(std::min(nt, cw::num_cus()));
+    Layout ly;
+    if (pick_layout(a.n, ly)) hipLaunchKernelGGL(k_block_fwd_c<true>, grid, dim3(FT), 0, s, a, ly);
     else hipLaunchKernelGGL(k_block_fwd_c<false>, grid, dim3(FT), 0, s, a, ly);
 }
 

@@ -159,6 +159,21 @@ struct FwdArgsC {
     int dn_log2, nn;       // next layer: log2 dilation, T / dilation
 };
 
+// column-owning bf16 block backward (block_bwd_bf16.hip)
+struct BwdArgsC {
+    unsigned long long* stamps;            // diagnostic builds (-DASTYLE_STAMPS) only
+    const u16* tin;        // d loss / d e_{l+1} incl. its direct term (chain, or D_{l+1} at the top)
+    const u16* dadd;       // D_l, the direct loss gradient of e_l (or null)
+    u16* gout;             // d loss / d e_l incl. D_l
+    const u16* wbf;        // [3 taps][4 q][8 kb][64 lanes][8] W_d A fragments:
+                           //   lane (m, h) element e = W_d[tap][ci = 32 q + m][co = 16 kb + 8 h + e]
+    const u16* wrb;        // [4 q][8 kb][64][8] W_r A fragments: W_r[co = 32 q + m][o = 16 kb + 8 h + e]
+    const uint16_t* mu;    // [B*T][2 h][4 q] u > 0 bits, this layer's positions
+    const uint16_t* me;    // [B*T][2][4] e_l > 0 bits, this layer's positions
+    const u16* zero;       // >= 256 zero bytes
+    int B, T, d, n;        // dilation, n = T / d
+};
+
 struct GramArgs {
     const void* act; size_t tstride;       // tensor u lives at act + uid[u] * tstride elements
     void* actw;                             // same base, writable (bwd, in place)
@@ -225,6 +240,7 @@ void launch_block_bwd(const BwdArgs& a, hipStream_t s);
 void launch_block_fwd_bf16(const FwdArgsB& a, hipStream_t s);
 void launch_block_bwd_bf16(const BwdArgsB& a, hipStream_t s);
 void launch_block_fwd_c(const FwdArgsC& a, hipStream_t s);
+void launch_block_bwd_c(const BwdArgsC& a, hipStream_t s);
 template <typename S>
 void launch_bottleneck_fwd(const S* e, float* y, const float* wb, const float* bb,
                            int B, int T, hipStream_t s);

@@ -290,6 +290,25 @@ def loss_and_grad(x, W, *, cont_ids, style_ids, phi_c, phi_s, lambd=100.0, gamma
     nb = needed_blocks(cont_ids, style_ids)
     ext, cache = encoder_forward(x, W, nb, need_bottleneck=31 in cont_ids, dtype=dtype)
     T = ext[0].shape[0]
+    content, style, grads = tap_terms(ext, cont_ids=cont_ids, style_ids=style_ids, phi_c=phi_c,
+                                      phi_s=phi_s, lambd=lambd, gatys=gatys,
+                                      nb_channels=nb_channels, cnt_channels=cnt_channels)
+    g = encoder_backward(cache, W, grads, dtype=dtype)
+    # TF evaluates the regulariser whatever gamma is (methods.py:121-125); its gradient
+    # enters only through gamma.
+    reg, greg = stft_reg(x) if x.shape[0] >= FRAME else (0.0, np.zeros(T))
+    if gamma != 0.0:
+        g = g + gamma * greg
+    total = content + lambd * style + gamma * reg
+    return np.array([total, content, style, reg]), g
+
+
+def tap_terms(ext, *, cont_ids, style_ids, phi_c, phi_s, lambd=100.0, gatys=False,
+              nb_channels=C, cnt_channels=C):
+    """Content and style terms of methods.py:116-119 and their gradients w.r.t. the extracts
+    (dict extract id -> [T, width]; the style part already scaled by lambd)."""
+    T = ext[0].shape[0]
+    dtype = ext[0].dtype
     grads = {}
     # content: 10 * mean((emb - phi_c)^2)                            methods.py:116-117
     emb = content_embeds(ext, cont_ids, cnt_channels)
@@ -322,14 +341,7 @@ def loss_and_grad(x, W, *, cont_ids, style_ids, phi_c, phi_s, lambd=100.0, gamma
         dstl = stl @ np.transpose(S, (0, 2, 1))
     for n_, i in enumerate(style_ids):
         grads[i] = grads.get(i, 0) + dstl[n_]
-    g = encoder_backward(cache, W, grads, dtype=dtype)
-    # TF evaluates the regulariser whatever gamma is (methods.py:121-125); its gradient
-    # enters only through gamma.
-    reg, greg = stft_reg(x) if x.shape[0] >= FRAME else (0.0, np.zeros(T))
-    if gamma != 0.0:
-        g = g + gamma * greg
-    total = content + lambd * style + gamma * reg
-    return np.array([total, content, style, reg]), g
+    return content, style, grads
 
 
 def targets_from_audio(W, content_wav_mu, style_wavs_mu, source_wavs_mu, *, cont_ids,

@@ -235,6 +235,50 @@ def test_bf16_loss_grad_close_to_oracle(tag, weights, golden, dev):
     assert cos >= 0.98 and rel(grad, ref_g) <= 0.25, (cos, rel(grad, ref_g))
 
 
+def _bf16(a):
+    """Round to bf16 (RNE) and back to float64."""
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16)
+    return t.to(torch.float32).numpy().astype(np.float64)
+
+
+@pytest.mark.parametrize('tag', ['c1', 'trunc', 'ours', 'gatys'])
+def test_bf16_backward_linearized(tag, weights, dev):
+    """The bf16 backward against the fp64 backward linearised at the GPU's own bf16 forward:
+    its activations (read back exactly), the relu patterns they imply, the bf16-rounded block
+    weights and the loss gradients of its own extracts.  What remains is the backward's own
+    rounding (g_u, D and the chain are stored in bf16), so a wrong halo row, mask bit, tap or
+    direct-gradient add at any dilation shows up far above the bound."""
+    T = 2048
+    kw = CASES[tag]
+    phi_c, phi_s = _targets(tag, T, weights)
+    x = O.mu_law_numpy(synthetic_clips(1, T, 42)[0]) + np.random.default_rng(5).normal(0, 4, T)
+    nb = O.needed_blocks(kw['cont_ids'], kw['style_ids'])
+    eng = _engine(1, T, kw, weights, precision='bf16')
+    xt = torch.tensor(x[None], dtype=torch.float32, device=dev)
+    eng.forward(xt)
+    ext = [eng.extract(i).cpu().numpy()[0].astype(np.float64) for i in range(nb)]
+    if nb == 30:
+        ext.append(ext[29])
+        if 31 in kw['cont_ids']:
+            ext.append(eng.extract(31).cpu().numpy()[0].astype(np.float64))
+    Wq = {k: (_bf16(v) if k.endswith('/W') and ('dilated' in k or 'res_' in k) else np.asarray(v, np.float64))
+          for k, v in weights.items()}
+    e0 = _bf16(O.conv1d_same((x / 128.0)[:, None], Wq['ae_startconv/W'], Wq['ae_startconv/biases'], 1))
+    es = [e0] + ext[:nb]
+    us = [O.conv1d_same(O.relu(es[l]), Wq['ae_dilatedconv_%d/W' % (l + 1)],
+                        Wq['ae_dilatedconv_%d/biases' % (l + 1)], O.dilation_of(l)) for l in range(nb)]
+    _, _, grads = O.tap_terms(ext, cont_ids=kw['cont_ids'], style_ids=kw['style_ids'], phi_c=phi_c,
+                              phi_s=phi_s, lambd=100.0, gatys=kw['gatys'],
+                              nb_channels=kw['nb_channels'], cnt_channels=kw['cnt_channels'])
+    ref = O.encoder_backward({'es': es, 'us': us, 'n_blocks': nb}, Wq, grads)
+    eng.set_targets(torch.tensor(phi_c, dtype=torch.float32), torch.tensor(phi_s, dtype=torch.float32))
+    _, grad = eng.loss_grad(xt)
+    grad = grad.cpu().numpy()[0]
+    e = rel(grad, ref)
+    print('%s bf16 backward vs linearised fp64: rel-L2 %.3g' % (tag, e))
+    assert e <= 1.5e-2, e
+
+
 @pytest.mark.parametrize('T', [512, 2048])
 def test_bf16_extracts_and_embeds(T, weights, dev):
     kw = dict(CASES['trunc'], cont_ids=[29, 31], style_ids=[0, 9, 30])

@@ -1,5 +1,8 @@
-"""Diagnostic: per-phase cycle shares of the bf16 block-forward kernel (s_memtime stamps,
-libastyle_stamps.so built with -DASTYLE_STAMPS).  Shares, not absolute time, are meaningful."""
+"""Diagnostic: per-phase cycle shares of the bf16 block kernels (s_memtime stamps,
+libastyle_stamps.so built with -DASTYLE_STAMPS).  Shares, not absolute time, are meaningful.
+
+usage: stamps.py [clips] [fwd|bwd]   (bwd runs one loss+grad; the forward kernel's slots are 0-2,
+the backward's 4-7)"""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ.setdefault('ASTYLE_LIB', os.path.join(ROOT, 'audio_style_transfer_amd', 'libastyle_stamps.so'))
@@ -8,20 +11,27 @@ import torch
 from audio_style_transfer_amd.engine import StyleEngine
 from audio_style_transfer_amd import _lib
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-eng = StyleEngine(B, 16384, [29], list(range(30)), precision='bf16')
-x = torch.randn(B, 16384, device='cuda') * 40
-eng.forward(x); torch.cuda.synchronize()
+mode = sys.argv[2] if len(sys.argv) > 2 else 'fwd'
+T = 16384
+eng = StyleEngine(B, T, [29], list(range(30)), precision='bf16')
+x = torch.randn(B, T, device='cuda') * 40
+if mode == 'bwd':
+    eng.set_targets(torch.randn(T, 128) * 0.1, torch.randn(*eng.style_shape) * 0.01)
+run = (lambda: eng.loss_grad(x)) if mode == 'bwd' else (lambda: eng.forward(x))
+run(); torch.cuda.synchronize()
 buf = torch.zeros(12, dtype=torch.int64, device='cuda')
 lib = _lib.load()
 lib.ast_debug_stamps.argtypes = [ctypes.c_void_p]
 lib.ast_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
-eng.forward(x); torch.cuda.synchronize()
+run(); torch.cuda.synchronize()
 lib.ast_debug_stamps(None)
 v = buf.cpu().tolist()
-names = ['loop-top vmcnt wait', 'barrier', 'DMA issue', 'GEMM1', 'epilogue1 + mu', 'GEMM2',
-         'epilogue2 + stores', '-', '-', '-', '-', '-']
-tot = sum(v)
-tiles = B * 16384 // 128 * 30 / 256   # tiles per CU over the 30 block launches
-for n, c in zip(names, v):
-    if c:
-        print('%-20s %6.1f %%   %8.0f cycles/tile/wave' % (n, 100.0 * c / tot, c / (4 * 256 * tiles)))
+names = ['fwd: top wait + barrier', 'fwd: GEMM1 + epi2 of prev + DMA', 'fwd: epi1 + GEMM2', '-',
+         'bwd: top wait + barrier', 'bwd: step 1 + g_u + barrier', 'bwd: step 2 + DMA',
+         'bwd: step 3 (mask, +tot, +D, stores)', '-', '-', '-', '-']
+tiles = B * T // 128 * 30 / 256   # tiles per CU over the 30 block launches
+for lo, hi in ((0, 4), (4, 8)):
+    tot = sum(v[lo:hi])
+    for n, c in zip(names[lo:hi], v[lo:hi]):
+        if c:
+            print('%-40s %6.1f %%   %8.0f cycles/tile/wave' % (n, 100.0 * c / tot, c / (4 * 256 * tiles)))
