@@ -44,15 +44,13 @@ constexpr size_t WD = 0, WDT = 3 * C * C, BD = 6 * C * C, WR = BD + C, WRT = WR 
 constexpr size_t WB_OFF = BLK_OFF + NBLK_MAX * BLK_SZ;   // [128][16]
 constexpr size_t BB_OFF = WB_OFF + C * 16;
 constexpr size_t W_TOTAL = BB_OFF + 16;
-// bf16 copies (precision 1), u16 elements per block
-constexpr size_t WDB = 0, WDTB = 3 * C * C, WRB = 6 * C * C, WRTB = 7 * C * C;
+// bf16 MFMA fragments (precision 1), u16 elements per block.
 // MFMA A-fragment order for block_fwd_bf16.hip: WFB [3 taps][4 q][8 kb][64 lanes][8],
 // lane (m, h) element e = W_d[tap][ci = 16 kb + 8 h + e][co = 32 q + m];
 // WRFB [4 q2][8 s][64][8], element e = W_r[co = kperm(s, h, e)][co2 = 32 q2 + m].
 // block_bwd_bf16.hip: WBFB [3][4 q][8 kb][64][8], element e = W_d[tap][32 q + m][16 kb + 8 h + e];
 // WRBFB [4 q][8 kb][64][8], element e = W_r[32 q + m][16 kb + 8 h + e]
-constexpr size_t WFB = 8 * C * C, WRFB = 11 * C * C, WBFB = 12 * C * C, WRBFB = 15 * C * C,
-                 BLKB_SZ = 16 * C * C;
+constexpr size_t WFB = 0, WRFB = 3 * C * C, WBFB = 4 * C * C, WRBFB = 7 * C * C, BLKB_SZ = 8 * C * C;
 inline int kperm(int s, int h, int e) { return 32 * (s >> 1) + 16 * (s & 1) + (e & 3) + 8 * (e >> 2) + 4 * h; }
 
 uint16_t host_bf16(float f) {   // round to nearest even
@@ -421,7 +419,6 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                                 hg[o] = hb[3 * C * C + (size_t)k * C * C + ci * C + co];
                             }
             u16* dst = x->wtsb + (size_t)(l - 1) * BLKB_SZ;
-            HIPCHK(hipMemcpy(dst + WDB, hb.data(), 6 * C * C * 2, hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(dst + WFB, hf.data(), 3 * C * C * 2, hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(dst + WBFB, hg.data(), 3 * C * C * 2, hipMemcpyHostToDevice));
             return 0;
@@ -450,7 +447,6 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                             hg[o] = hb[C * C + (size_t)(16 * st + 8 * (ln >> 5) + e) * C + 32 * q2 + (ln & 31)];
                         }
             u16* dst = x->wtsb + (size_t)(l - 1) * BLKB_SZ;
-            HIPCHK(hipMemcpy(dst + WRB, hb.data(), 2 * C * C * 2, hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(dst + WRFB, hf.data(), C * C * 2, hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(dst + WRBFB, hg.data(), C * C * 2, hipMemcpyHostToDevice));
             return 0;

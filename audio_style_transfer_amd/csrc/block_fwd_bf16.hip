@@ -21,8 +21,7 @@
 //    re-read of the row's first chunk.
 //  * relu masks leave as 16-bit words in the accumulator layout (bit mbit(i) = element i of one
 //    lane's 32x32 tile, common.h): u > 0 by this layer's position, e_{l+1} > 0 by the NEXT layer's
-//    position, so the backward applies them with no bit shuffling (block_bwd in
-//    encoder_bf16.hip).
+//    position, so the backward applies them with no bit shuffling (block_bwd_bf16.hip).
 #include "colwave.h"
 #include <algorithm>
 #include <type_traits>
@@ -109,11 +108,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, Layout ly) {
         for (int k = 0; k < 4; ++k) {
             const uint4 v = lds16(stg + (8 * k + (lane >> 3)) * SRB + (lane & 7) * 16);
             const int tt = ctime(t, 32 * w + 8 * k + (lane >> 3), otoff[k]);
-#ifndef ABL_NOSTORE
             *reinterpret_cast<uint4*>(a.eout + ((size_t)t.b * a.T + tt) * C + 64 * rho + (lane & 7) * 8) = v;
-#else
-            if (v.x == 0x12345u && tt < 0) *reinterpret_cast<uint4*>(a.eout) = v;
-#endif
         }
     };
     auto me_store = [&](const Tile& t, const uint32_t (&meb)[4]) {
@@ -210,11 +205,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, Layout ly) {
                 // 32-channel tile q2 in steps 3 q2 .. 3 q2 + 2, staging + whole-row stores in
                 // steps 15-22) and the next tile's DMA (steps 0-7, 16, 17, where the steps carry
                 // the fewest LDS reads).  The stores stay behind the last DMA (vmcnt(9) above).
-#ifndef ABL_NODMA
                 if (st < 4) { dma_slot(2 * st); dma_slot(2 * st + 1); }
                 if (st == 4) dma_slot(8);
-#endif
-#ifndef ABL_NOEPI2
                 if (PREV) {
                     // tile q2 = 0, 1 in steps 0-5, staged at 6, stored at 10; q2 = 2, 3 in steps
                     // 7-9 and 11-13, staged at 15, stored at 18
@@ -232,7 +224,6 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, Layout ly) {
                     if (st == 15) epi2_stage(1, opk);
                     if (st == 18) epi2_store(1, prev);
                 }
-#endif
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA

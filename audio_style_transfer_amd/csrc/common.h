@@ -11,7 +11,8 @@
 //                           are one contiguous run) as u16 words [h][q] in the 32x32 MFMA
 //                           accumulator layout: bit i of word (h, q) is channel
 //                           32 q + (i & 3) + 8 (i >> 2) + 4 h
-//   chain [2][B][T][C]      fp32 backward ping-pong (d loss / d e_l)
+//   chain [2][B][T][C]      backward ping-pong, storage type (d loss / d e_l; the bf16 chain
+//                           has the direct loss gradient D_l already added)
 // Dilated rows are visited in time_to_batch order (masked.py:57-86): tile position p maps to
 // time t = (p % n) * d + p / n with n = T / d, so a tile's tap neighbours are p-1 / p+1 and
 // the halo is 2 rows at every dilation.
@@ -126,25 +127,6 @@ struct BwdArgs {
     int B, T, d, n;
 };
 
-struct FwdArgsB {
-    unsigned long long* stamps;            // diagnostic builds (-DASTYLE_STAMPS) only
-    const u16* ein; u16* eout;
-    const u16* wdT; const float* bd;       // wdT [3][co][ci] bf16
-    const u16* wrT; const float* br;       // wrT [co][ci] bf16
-    uint32_t* mu; uint32_t* me;
-    int B, T, d, n;
-};
-
-struct BwdArgsB {
-    unsigned long long* stamps;            // diagnostic builds (-DASTYLE_STAMPS) only
-    const u16* gin; const u16* din; u16* gout;
-    const u16* wr;     // [ci][co] bf16  (A operand of step 1)
-    const float* wr32; // [ci][co] fp32  (halo rows)
-    const u16* wd;     // [3][ci][co] bf16 (A operand of step 2)
-    const uint32_t* mu; const uint32_t* me;
-    int B, T, d, n;
-};
-
 // column-owning bf16 block forward (block_fwd_bf16.hip)
 struct FwdArgsC {
     unsigned long long* stamps;            // diagnostic builds (-DASTYLE_STAMPS) only
@@ -237,8 +219,6 @@ void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T,
                           hipStream_t s);
 void launch_block_fwd(const FwdArgs& a, hipStream_t s);
 void launch_block_bwd(const BwdArgs& a, hipStream_t s);
-void launch_block_fwd_bf16(const FwdArgsB& a, hipStream_t s);
-void launch_block_bwd_bf16(const BwdArgsB& a, hipStream_t s);
 void launch_block_fwd_c(const FwdArgsC& a, hipStream_t s);
 void launch_block_bwd_c(const BwdArgsC& a, hipStream_t s);
 template <typename S>
