@@ -15,10 +15,12 @@ SOURCES = ['encoder.hip', 'block_fwd_bf16.hip', 'block_bwd_bf16.hip', 'gram.hip'
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall',
          '-Wno-unused-function', '-munsafe-fp-atomics']
-# per-source extras: the column-owning block kernels keep their weights in AGPRs (asm-loaded)
-# and need the MFMA accumulators in arch VGPRs, where the epilogues read them without copies
-EXTRA = {'block_fwd_bf16.hip': ['-mllvm', '-amdgpu-mfma-vgpr-form=1'],
-         'block_bwd_bf16.hip': ['-mllvm', '-amdgpu-mfma-vgpr-form=1']}
+# per-source extras: the column-owning block kernels keep their weights in AGPRs and need the
+# MFMA accumulators in arch VGPRs, where the epilogues read them without copies; their fully
+# unrolled tile loops exceed the default pragma-unroll size limit (a partly unrolled loop would
+# index the register-resident weight arrays dynamically and demote them to scratch)
+_CW = ['-mllvm', '-amdgpu-mfma-vgpr-form=1', '-mllvm', '-pragma-unroll-threshold=1000000']
+EXTRA = {'block_fwd_bf16.hip': _CW, 'block_bwd_bf16.hip': _CW}
 
 
 def _stale() -> bool:
