@@ -271,7 +271,11 @@ StyleArgs style_args(ast_ctx* x) {
     memset(&a, 0, sizeof(a));
     a.gpart = x->gpart; a.nchunk = x->nchunk;
     a.L = x->L; a.nu = x->nu;
-    for (int i = 0; i < x->L; ++i) a.lmap[i] = x->lmap[i];
+    a.lmap_identity = 1;
+    for (int i = 0; i < x->L; ++i) {
+        a.lmap[i] = x->lmap[i];
+        if (x->lmap[i] != i) a.lmap_identity = 0;
+    }
     a.nb = std::min(x->cfg.nb_channels, C);
     a.coef = x->cfg.lambd * 1e3f * 2.0f / (float)(a.nb * x->L * x->L);
     a.B = x->cfg.batch;

@@ -170,6 +170,7 @@ struct GramArgs {
 struct StyleArgs {
     const float* gpart; int nchunk;
     int L; int lmap[32]; int nu;
+    int lmap_identity;                      // lmap[i] == i for every tap (no S~ fold needed)
     const float* phi; size_t phi_bstride;   // elements between clips (0 = shared)
     int nb; float coef;                     // coef = lambd * 1e3 * 2 / (nb * L * L)
     float* smat; float* spart;              // [B][C][32][32], [B][C]

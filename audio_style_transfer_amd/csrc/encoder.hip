@@ -266,36 +266,63 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
     }
 }
 
-// d loss / d x = (1/128) sum_k sum_c W0[k][c] g0[t-k+1][c]; one wave per sample.
+// d loss / d x (startconv transposed, model.py:82-93, incl. the 1/128 of model.py:83):
+//   gx[t] = (1/128) sum_k a_k[t - k + 1],   a_k[t] = sum_c W0[k][c] g0[t][c].
+// One workgroup per SCB rows: the 16-B chunks of a row go to CPR consecutive lanes, which form
+// the row's three dot products (shuffle-reduced); each row of g0 is read once, in whole lines.
+constexpr int SCB = 256;
 template <typename S>
 __global__ void __launch_bounds__(256) k_startconv_bwd(const S* __restrict__ g0,
                                                        float* __restrict__ gx,
                                                        const float* __restrict__ w0, int B,
                                                        int T) {
-    const size_t wid = ((size_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    if (wid >= (size_t)B * T) return;
-    const int t = (int)(wid % T);
-    const S* base = g0 + (wid - t) * C;
-    float s = 0.f;
+    constexpr int EPC = 16 / (int)sizeof(S);   // elements per 16-B chunk
+    constexpr int CPR = C / EPC;               // chunks (lanes) per row
+    constexpr int RPP = 256 / CPR;             // rows per pass
+    __shared__ float A[3][SCB + 2];            // a_k of rows t0 - 1 .. t0 + SCB
+    const int tiles = T / SCB;
+    const int b = blockIdx.x / tiles, t0 = (blockIdx.x - b * tiles) * SCB;
+    const int tid = threadIdx.x, ch = tid % CPR;
+    float w[3][EPC];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int tt = t - k + 1;
-        if (tt < 0 || tt >= T) continue;
-        float g0v, g1v;
-        if constexpr (sizeof(S) == 4) {
-            const float2 gv = *reinterpret_cast<const float2*>(base + (size_t)tt * C + 2 * lane);
-            g0v = gv.x; g1v = gv.y;
-        } else {
-            const uint32_t gv = *reinterpret_cast<const uint32_t*>(base + (size_t)tt * C + 2 * lane);
-            g0v = bflo(gv); g1v = bfhi(gv);
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) w[k][e] = w0[k * C + ch * EPC + e];
+    const S* base = g0 + (size_t)b * T * C + ch * EPC;
+    for (int i = tid / CPR; i < SCB + 2; i += RPP) {
+        const int t = t0 - 1 + i;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+        if (t >= 0 && t < T) {
+            const uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)t * C);
+            const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+            float x[EPC];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if constexpr (sizeof(S) == 4) {
+                    x[k] = __uint_as_float(u[k]);
+                } else {
+                    x[2 * k] = bflo(u[k]);
+                    x[2 * k + 1] = bfhi(u[k]);
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < EPC; ++e) {
+                s0 = fmaf(w[0][e], x[e], s0);
+                s1 = fmaf(w[1][e], x[e], s1);
+                s2 = fmaf(w[2][e], x[e], s2);
+            }
         }
-        s = fmaf(w0[k * C + 2 * lane], g0v, s);
-        s = fmaf(w0[k * C + 2 * lane + 1], g1v, s);
-    }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0) gx[wid] = s / 128.0f;
+        for (int off = CPR / 2; off > 0; off >>= 1) {
+            s0 += __shfl_xor(s0, off);
+            s1 += __shfl_xor(s1, off);
+            s2 += __shfl_xor(s2, off);
+        }
+        if (ch == 0) { A[0][i] = s0; A[1][i] = s1; A[2][i] = s2; }
+    }
+    __syncthreads();
+    for (int i = tid; i < SCB; i += 256)   // t = t0 + i is image row i + 1
+        gx[(size_t)b * T + t0 + i] = (A[0][i + 2] + A[1][i + 1] + A[2][i]) / 128.0f;
 }
 
 // ae_bottleneck (model.py:121-127): 1x1, 128 -> 16.  Thread per (row, out channel).
@@ -352,8 +379,7 @@ void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b
 }
 template <typename S>
 void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T, hipStream_t s) {
-    const size_t n = (size_t)B * T * 64;
-    hipLaunchKernelGGL(k_startconv_bwd<S>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g0,
+    hipLaunchKernelGGL(k_startconv_bwd<S>, dim3((unsigned)(B * (T / SCB))), dim3(256), 0, s, g0,
                        gx, w0, B, T);
 }
 template <typename S>

@@ -154,15 +154,15 @@ __global__ void __launch_bounds__(256) k_style_ours(StyleArgs a) {
     }
     __syncthreads();
     float g[16];
+    int li[16], l2i[16];         // (l, l2) of element e = lane + 64 k (one division per element)
     float ss = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int e = lane + 64 * k;
+        li[k] = e / L;
+        l2i[k] = e - li[k] * L;
         g[k] = 0.f;
-        if (e < L * L) {
-            const int l = e / L, l2 = e - l * L;
-            g[k] = Gu[w][a.lmap[l] * 33 + a.lmap[l2]];
-        }
+        if (e < L * L) g[k] = Gu[w][a.lmap[li[k]] * 33 + a.lmap[l2i[k]]];
         ss = fmaf(g[k], g[k], ss);
     }
     ss = wave_sum(ss);
@@ -192,19 +192,17 @@ __global__ void __launch_bounds__(256) k_style_ours(StyleArgs a) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int e = lane + 64 * k;
-        if (e < L * L) {
-            const int l = e / L, l2 = e - l * L;
-            dG[w][l * 33 + l2] = dgn[k] * inv - big * (g[k] * inv) * dot * inv;
-        }
+        if (e < L * L) dG[w][li[k] * 33 + l2i[k]] = dgn[k] * inv - big * (g[k] * inv) * dot * inv;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int e = lane + 64 * k;
         if (e < L * L) {
-            const int l = e / L, l2 = e - l * L;
+            const int l = li[k], l2 = l2i[k];
             const float sv = dG[w][l * 33 + l2] + dG[w][l2 * 33 + l];
-            atomicAdd(&St[w][a.lmap[l] * 32 + a.lmap[l2]], sv);
+            if (a.lmap_identity) St[w][l * 32 + l2] = sv;     // every tap its own tensor
+            else atomicAdd(&St[w][a.lmap[l] * 32 + a.lmap[l2]], sv);
         }
     }
     __syncthreads();
@@ -251,6 +249,61 @@ __global__ void __launch_bounds__(256) k_content(ContentArgs a) {
         a.lpart[(size_t)b * a.lstride + (blockIdx.x - b * tilesPer)] = red[0] + red[1] + red[2] + red[3];
 }
 
+// Same for the common bf16 case (128-channel tap, bf16 e and cg, ncol a multiple of 8, no emb
+// copy): one thread per 16-B chunk of e / cg, the matching 32 B of phi as two float4.
+__global__ void __launch_bounds__(256) k_content_bf16x8(ContentArgs a) {
+    __shared__ float red[4];
+    const u16* E = (const u16*)a.e;
+    u16* CG = (u16*)a.cg;
+    const int tilesPer = a.T / CROWS;
+    const int b = blockIdx.x / tilesPer;
+    const int t0 = (blockIdx.x - b * tilesPer) * CROWS;
+    const int tid = threadIdx.x;
+    float sd = 0.f;
+#pragma unroll
+    for (int it = 0; it < CROWS * (C / 8) / 256; ++it) {
+        const int i = it * 256 + tid;
+        const int tt = i >> 4, ch = i & 15;
+        const size_t row = (size_t)b * a.T + t0 + tt;
+        const uint4 ev = *reinterpret_cast<const uint4*>(E + row * C + ch * 8);
+        float d[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (ch * 8 < a.ncol && a.phi) {
+            const float* ph = a.phi + (size_t)b * a.phi_bstride + (size_t)(t0 + tt) * a.ncc + a.off + ch * 8;
+            const float4 p0 = *reinterpret_cast<const float4*>(ph);
+            const float4 p1 = *reinterpret_cast<const float4*>(ph + 4);
+            const float pv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+            const uint32_t eu[4] = {ev.x, ev.y, ev.z, ev.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                d[2 * k] = bflo(eu[k]) - pv[2 * k];
+                d[2 * k + 1] = bfhi(eu[k]) - pv[2 * k + 1];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sd = fmaf(d[k], d[k], sd);
+        }
+        if (CG) {
+            uint32_t o[4];
+            u16* cp = CG + row * C + ch * 8;
+            if (a.accumulate) {
+                const uint4 old = *reinterpret_cast<const uint4*>(cp);
+                const uint32_t ou[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    o[k] = pack2(bflo(ou[k]) + a.coef * d[2 * k], bfhi(ou[k]) + a.coef * d[2 * k + 1]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) o[k] = pack2(a.coef * d[2 * k], a.coef * d[2 * k + 1]);
+            }
+            *reinterpret_cast<uint4*>(cp) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+    }
+    sd = wave_sum(sd);
+    if ((tid & 63) == 0) red[tid >> 6] = sd;
+    __syncthreads();
+    if (tid == 0 && a.lpart)
+        a.lpart[(size_t)b * a.lstride + (blockIdx.x - b * tilesPer)] = red[0] + red[1] + red[2] + red[3];
+}
+
 // parts[b] = (content + lambd*style, content, style, 0)
 __global__ void __launch_bounds__(256) k_finalize(float* parts, const float* cpart, int ncpart,
                                                   float cscale, const float* spart, int nspart,
@@ -287,7 +340,10 @@ void launch_style_ours(const StyleArgs& a, hipStream_t s) {
 }
 void launch_content(const ContentArgs& a, hipStream_t s) {
     const dim3 g(a.B * (a.T / CROWS));
-    if (a.e_bf16 && a.cg_bf16) hipLaunchKernelGGL((k_content<u16, u16>), g, dim3(256), 0, s, a);
+    const bool x8 = a.e_bf16 && a.cg_bf16 && a.W == C && a.ncol % 8 == 0 && a.off % 4 == 0 &&
+                    a.ncc % 4 == 0 && !a.embc;
+    if (x8) hipLaunchKernelGGL(k_content_bf16x8, g, dim3(256), 0, s, a);
+    else if (a.e_bf16 && a.cg_bf16) hipLaunchKernelGGL((k_content<u16, u16>), g, dim3(256), 0, s, a);
     else if (a.e_bf16) hipLaunchKernelGGL((k_content<u16, float>), g, dim3(256), 0, s, a);
     else if (a.cg_bf16) hipLaunchKernelGGL((k_content<float, u16>), g, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_content<float, float>), g, dim3(256), 0, s, a);
