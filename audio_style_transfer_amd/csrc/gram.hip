@@ -141,7 +141,10 @@ __global__ void __launch_bounds__(256) k_style_ours(StyleArgs a) {
     __shared__ float Gu[4][32 * 33];
     __shared__ float dG[4][32 * 33];
     __shared__ float St[4][32 * 32];
+    __shared__ int lm[32];              // tap -> unique tensor (a by-value kernel-argument array
+                                        // indexed at run time would live in scratch)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid < 32) lm[tid] = a.lmap[tid];
     const int b = blockIdx.x / (C / 4);
     const int c = (blockIdx.x % (C / 4)) * 4 + w;
     const int L = a.L;
@@ -162,7 +165,7 @@ __global__ void __launch_bounds__(256) k_style_ours(StyleArgs a) {
         li[k] = e / L;
         l2i[k] = e - li[k] * L;
         g[k] = 0.f;
-        if (e < L * L) g[k] = Gu[w][a.lmap[li[k]] * 33 + a.lmap[l2i[k]]];
+        if (e < L * L) g[k] = Gu[w][lm[li[k]] * 33 + lm[l2i[k]]];
         ss = fmaf(g[k], g[k], ss);
     }
     ss = wave_sum(ss);
@@ -202,7 +205,7 @@ __global__ void __launch_bounds__(256) k_style_ours(StyleArgs a) {
             const int l = li[k], l2 = l2i[k];
             const float sv = dG[w][l * 33 + l2] + dG[w][l2 * 33 + l];
             if (a.lmap_identity) St[w][l * 32 + l2] = sv;     // every tap its own tensor
-            else atomicAdd(&St[w][a.lmap[l] * 32 + a.lmap[l2]], sv);
+            else atomicAdd(&St[w][lm[l] * 32 + lm[l2]], sv);
         }
     }
     __syncthreads();
