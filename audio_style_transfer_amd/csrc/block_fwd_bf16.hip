@@ -140,10 +140,11 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, Layout ly) {
         constexpr bool PREV = decltype(has_prev)::value;
         const int cur = it & 1;
         const Tile cu = tile_of(tile);
-        // this wave's DMA of the current image is complete (only the <= 10 stores of the
-        // previous tile, issued after it, may still be in flight: vmcnt counts in issue order);
-        // the barrier publishes every wave's part and retires all reads of the other image
-        if (PREV) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        // this wave's DMA of the current image is complete: vmcnt counts in issue order, and
+        // only 5 stores follow the last DMA slot (step 16) of the previous iteration: the second
+        // half's 4 row stores (step 18) and the u > 0 mask store of phase B; the barrier
+        // publishes every wave's part and retires all reads of the other image
+        if (PREV) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -203,10 +204,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, Layout ly) {
                 // side work, spread so that every step carries a few independent instructions
                 // between its MFMAs: epilogue 2 of the previous tile (pack / mask bits / swap of
                 // 32-channel tile q2 in steps 3 q2 .. 3 q2 + 2, staging + whole-row stores in
-                // steps 15-22) and the next tile's DMA (steps 0-7, 16, 17, where the steps carry
-                // the fewest LDS reads).  The stores stay behind the last DMA (vmcnt(9) above).
-                if (st < 4) { dma_slot(2 * st); dma_slot(2 * st + 1); }
-                if (st == 4) dma_slot(8);
+                // steps 6-18) and the next tile's DMA (one slot every other step, 0-16).  The wait
+                // at the top counts what follows the last slot (vmcnt(5)).
+                if (st % 2 == 0 && st / 2 < DPW) dma_slot(st / 2);   // one slot every other step
                 if (PREV) {
                     // tile q2 = 0, 1 in steps 0-5, staged at 6, stored at 10; q2 = 2, 3 in steps
                     // 7-9 and 11-13, staged at 15, stored at 18
