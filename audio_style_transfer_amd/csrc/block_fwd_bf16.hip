@@ -178,9 +178,18 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, Layout ly) {
         uint32_t o2[8];
         {
             auto bload = [&](int st) { return lds16(xb + (st >> 3) * RSB + (st & 7) * 32); };
+            // B fragment of step st: relu'd (and tap-masked) one step ahead, so no MFMA waits on
+            // the VALU that forms its operand
+            auto bprep = [&](int st, uint4 v) {
+                const int tp = st >> 3;
+                v = relu8(v);
+                if (MASKED && ((tp == 0 && !ok0) || (tp == 2 && !ok2))) v = make_uint4(0, 0, 0, 0);
+                return v;
+            };
             uint4 bl[3], al[2][4];
             bl[0] = bload(0);
             bl[1] = bload(1);
+            uint4 bn = bprep(0, bl[0]);
 #pragma unroll
             for (int st = 0; st < 24; ++st) {
                 const int tp = st >> 3, kb = st & 7;
@@ -189,8 +198,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, Layout ly) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) al[(st + 1) & 1][q] = W1[(q * 8 + ((st + 1) & 7)) * 64 + lane];
                 }
-                uint4 bv = relu8(bl[st % 3]);
-                if (MASKED && ((tp == 0 && !ok0) || (tp == 2 && !ok2))) bv = make_uint4(0, 0, 0, 0);
+                const uint4 bv = bn;
+                if (st + 1 < 24) bn = bprep(st + 1, bl[(st + 1) % 3]);
                 if (tp == 0) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) acc[q] = mfma_bf16(wr0[q][kb], bv, acc[q]);
