@@ -42,6 +42,15 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_c(BwdArgsC a, Layout ly) {
     const int r = lane & 31, h = lane >> 5;
 
     // ---- per-launch setup (as the forward: taps 0 / 2 in AGPRs, tap 1 and W_r in LDS) --------
+    // the first tile's image streams in while the weights load (it only touches XS[0])
+    ImageDma<MASKED> dma;
+    dma.init(w, lane, ly, a.d);
+    if (blockIdx.x < ntiles) {
+        dma.aim(a.tin, tile_at<MASKED>(blockIdx.x, tiles, a.n, a.d, ly), ly, a.T, a.n);
+        const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[0][0] + (uint32_t)(w * 1024);
+#pragma unroll
+        for (int j = 0; j < DPW; ++j) dma.issue(j, a.tin, a.zero, lds0, a.T, a.n, a.d);
+    }
     uint4 wr0[4][8], wr2[4][8];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -64,8 +73,6 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_c(BwdArgsC a, Layout ly) {
     const int c = 32 * w + r;                // this lane's tile column
     const int Lc = frow(c, ly);
     const bool onesg = ly.M == TMB;          // halo rows are real positions (else zero pad rows)
-    ImageDma<MASKED> dma;
-    dma.init(w, lane, ly, a.d);
     // staged output / D rows: piece k of a half is wave column 8 k + lane / 8
     int otoff[4];
 #pragma unroll
@@ -94,14 +101,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_c(BwdArgsC a, Layout ly) {
     };
 
     Masks mk{};
-    if (blockIdx.x < ntiles) {                // prologue: the first tile's image and masks
-        const Tile t0 = tile_of(blockIdx.x);
-        mk = load_masks(t0);
-        dma.aim(a.tin, t0, ly, a.T, a.n);
-        const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[0][0] + (uint32_t)(w * 1024);
-#pragma unroll
-        for (int j = 0; j < DPW; ++j) dma.issue(j, a.tin, a.zero, lds0, a.T, a.n, a.d);
-    }
+    if (blockIdx.x < ntiles) mk = load_masks(tile_of(blockIdx.x));   // the first tile's masks
     STAMP_DECL
     int it = 0;
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {

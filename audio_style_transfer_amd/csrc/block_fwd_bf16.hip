@@ -45,6 +45,15 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, Layout ly) {
     const int r = lane & 31, h = lane >> 5;
 
     // ---- per-launch setup -------------------------------------------------------------
+    // the first tile's image streams in while the weights load (it only touches XS[0])
+    ImageDma<MASKED> dma;
+    dma.init(w, lane, ly, a.d);
+    if (blockIdx.x < ntiles) {
+        dma.aim(a.ein, tile_at<MASKED>(blockIdx.x, tiles, a.n, a.d, ly), ly, a.T, a.n);
+        const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[0][0] + (uint32_t)(w * 1024);
+#pragma unroll
+        for (int j = 0; j < DPW; ++j) dma.issue(j, a.ein, a.zero, lds0, a.T, a.n, a.d);
+    }
     // taps 0 and 2 live in the accumulator register file (MFMA A operands may be AGPRs): the
     // arch VGPRs stay free for accumulators, fragments and addresses.  Plain loads (the compiler
     // counts them), then a tied no-op asm that pins each fragment to AGPRs.
@@ -68,8 +77,6 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, Layout ly) {
     const int c = 32 * w + r;                  // this lane's tile column
     const int Lc = frow(c, ly);
     const int tcoff = MASKED ? 0 : row_toff(Lc, ly, a.d);
-    ImageDma<MASKED> dma;
-    dma.init(w, lane, ly, a.d);
     __syncthreads();
 
     // staged output rows: piece k of a round is wave column 8 k + lane / 8
@@ -120,12 +127,6 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_c(FwdArgsC a, Layout ly) {
         }
     };
 
-    if (blockIdx.x < ntiles) {                  // prologue: the first tile's image
-        dma.aim(a.ein, tile_of(blockIdx.x), ly, a.T, a.n);
-        const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[0][0] + (uint32_t)(w * 1024);
-#pragma unroll
-        for (int j = 0; j < DPW; ++j) dma.issue(j, a.ein, a.zero, lds0, a.T, a.n, a.d);
-    }
     f32x16 acc[4];                 // GEMM 1 accumulators
     f32x16 acc2[4];                 // GEMM 2 accumulators, carried into the next iteration
     Tile prev{0, 0, 0};
