@@ -141,13 +141,15 @@ __global__ void __launch_bounds__(256) k_style_ours(StyleArgs a) {
     __shared__ float Gu[4][32 * 33];
     __shared__ float dG[4][32 * 33];
     __shared__ float St[4][32 * 32];
+    __shared__ uint16_t EL[1024];       // list element e -> (l << 8) | l2 (one division per block)
     __shared__ int lm[32];              // tap -> unique tensor (a by-value kernel-argument array
                                         // indexed at run time would live in scratch)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int L = a.L, LL = L * L;
     if (tid < 32) lm[tid] = a.lmap[tid];
+    for (int e = tid; e < LL; e += 256) EL[e] = (uint16_t)(((e / L) << 8) | (e % L));
     const int b = blockIdx.x / (C / 4);
     const int c = (blockIdx.x % (C / 4)) * 4 + w;
-    const int L = a.L;
     for (int e = lane; e < 1024; e += 64) {
         float s = 0.f;
         for (int ch = 0; ch < a.nchunk; ++ch)
@@ -156,57 +158,54 @@ __global__ void __launch_bounds__(256) k_style_ours(StyleArgs a) {
         St[w][e] = 0.f;
     }
     __syncthreads();
-    float g[16];
-    int li[16], l2i[16];         // (l, l2) of element e = lane + 64 k (one division per element)
+    // the list Gram is re-read from LDS wherever needed: per-lane copies of the <= 16
+    // elements a lane owns would cost ~250 registers and one wave per SIMD
+    auto gval = [&](int e) {
+        const uint32_t el = EL[e];
+        return Gu[w][lm[el >> 8] * 33 + lm[el & 255]];
+    };
+    auto lidx = [&](int e) {
+        const uint32_t el = EL[e];
+        return (int)(el >> 8) * 33 + (int)(el & 255);
+    };
     float ss = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int e = lane + 64 * k;
-        li[k] = e / L;
-        l2i[k] = e - li[k] * L;
-        g[k] = 0.f;
-        if (e < L * L) g[k] = Gu[w][lm[li[k]] * 33 + lm[l2i[k]]];
-        ss = fmaf(g[k], g[k], ss);
+    for (int e = lane; e < LL; e += 64) {
+        const float g = gval(e);
+        ss = fmaf(g, g, ss);
     }
     ss = wave_sum(ss);
     const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
     const bool active = c < a.nb;
-    const float* phi = a.phi ? a.phi + (size_t)b * a.phi_bstride + (size_t)c * L * L : nullptr;
+    const float* phi = a.phi ? a.phi + (size_t)b * a.phi_bstride + (size_t)c * LL : nullptr;
     float sd = 0.f, dot = 0.f;
-    float dgn[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int e = lane + 64 * k;
-        dgn[k] = 0.f;
-        if (e < L * L && active) {
-            const float gn = g[k] * inv;
-            if (a.embs) a.embs[(((size_t)b * a.nb) + c) * L * L + e] = gn;
-            if (a.phi) {
+    for (int e = lane; e < LL; e += 64) {     // d loss / d Gn (raw), loss partial, <Gn, dGn>
+        float dgn = 0.f;
+        if (active) {
+            const float gn = gval(e) * inv;
+            if (a.embs) a.embs[(((size_t)b * a.nb) + c) * LL + e] = gn;
+            if (phi) {
                 const float diff = gn - phi[e];
                 sd = fmaf(diff, diff, sd);
-                dgn[k] = a.coef * diff;
-                dot = fmaf(gn, dgn[k], dot);
+                dgn = a.coef * diff;
+                dot = fmaf(gn, dgn, dot);
             }
         }
+        dG[w][lidx(e)] = dgn;
     }
     sd = wave_sum(sd);
     dot = wave_sum(dot);
     const float big = ss >= 1e-12f ? 1.f : 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int e = lane + 64 * k;
-        if (e < L * L) dG[w][li[k] * 33 + l2i[k]] = dgn[k] * inv - big * (g[k] * inv) * dot * inv;
+    for (int e = lane; e < LL; e += 64) {     // l2-normalise backward (each lane its own elements)
+        const int i = lidx(e);
+        dG[w][i] = dG[w][i] * inv - big * (gval(e) * inv) * dot * inv;
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int e = lane + 64 * k;
-        if (e < L * L) {
-            const int l = li[k], l2 = l2i[k];
-            const float sv = dG[w][l * 33 + l2] + dG[w][l2 * 33 + l];
-            if (a.lmap_identity) St[w][l * 32 + l2] = sv;     // every tap its own tensor
-            else atomicAdd(&St[w][lm[l] * 32 + lm[l2]], sv);
-        }
+    for (int e = lane; e < LL; e += 64) {     // S = dG + dG^T folded onto unique tensors
+        const uint32_t el = EL[e];
+        const int l = el >> 8, l2 = el & 255;
+        const float sv = dG[w][l * 33 + l2] + dG[w][l2 * 33 + l];
+        if (a.lmap_identity) St[w][l * 32 + l2] = sv;     // every tap its own tensor
+        else atomicAdd(&St[w][lm[l] * 32 + lm[l2]], sv);
     }
     __syncthreads();
     if (a.smat) {
