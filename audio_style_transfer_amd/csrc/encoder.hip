@@ -224,61 +224,66 @@ __global__ void __launch_bounds__(256) k_block_bwd(BwdArgs a) {
 
 // ae_startconv (model.py:88-93): 1 -> 128 channels, K=3, d=1, input x/128 (model.py:82).
 // Thread per (row, 8 channels): 16-B bf16 (32-B fp32) stores, 16 lanes per row.
+constexpr int SFR = 256;   // rows per workgroup
 template <typename S>
 __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__ x,
                                                        S* __restrict__ e0,
                                                        const float* __restrict__ w0,
                                                        const float* __restrict__ b0, int B,
                                                        int T, uint16_t* __restrict__ me0) {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;   // (row, 8 channels)
-    const size_t rowi = i >> 4;
-    if (rowi >= (size_t)B * T) return;                         // B * T is a multiple of 16
-    const int m = (int)(i & 15);
-    const int t = (int)(rowi % T);
-    const float* xr = x + (rowi - t);
-    const float xm = t > 0 ? xr[t - 1] / 128.0f : 0.f;
-    const float x0 = xr[t] / 128.0f;
-    const float xp = t < T - 1 ? xr[t + 1] / 128.0f : 0.f;
-    float o[8];
+    // SFR rows per workgroup, 16 lanes per row; this lane's 8 channels' weights load once
+    const int m = threadIdx.x & 15;
+    float wk[3][8], bk[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const int c = m * 8 + j;
-        o[j] = (w0[c] * xm + w0[C + c] * x0 + w0[2 * C + c] * xp) + b0[c];
+        wk[0][j] = w0[m * 8 + j]; wk[1][j] = w0[C + m * 8 + j]; wk[2][j] = w0[2 * C + m * 8 + j];
+        bk[j] = b0[m * 8 + j];
     }
-    if constexpr (sizeof(S) == 4) {
-        float4* dst = reinterpret_cast<float4*>(e0 + rowi * C + m * 8);
-        dst[0] = make_float4(o[0], o[1], o[2], o[3]);
-        dst[1] = make_float4(o[4], o[5], o[6], o[7]);
-    } else {
-        uint32_t p[4];
+    for (int it = 0; it < SFR / 16; ++it) {
+        const size_t rowi = (size_t)blockIdx.x * SFR + it * 16 + (threadIdx.x >> 4);
+        const int t = (int)(rowi % T);
+        const float* xr = x + (rowi - t);
+        const float xm = t > 0 ? xr[t - 1] / 128.0f : 0.f;
+        const float x0 = xr[t] / 128.0f;
+        const float xp = t < T - 1 ? xr[t + 1] / 128.0f : 0.f;
+        float o[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) p[k] = pack2(o[2 * k], o[2 * k + 1]);
-        *reinterpret_cast<uint4*>(e0 + rowi * C + m * 8) = make_uint4(p[0], p[1], p[2], p[3]);
-        if (me0) {
-            // e_0 > 0 bits for block 0's backward (dilation 1: position = time) in the MFMA
-            // accumulator layout (common.h): channel 32 Q + 8 g + 4 h + j is element
-            // i = 4 g + j of word (h, Q), at bit mbit(i); this lane holds Q = m / 4, g = m % 4,
-            // h = 0 (p[0], p[1]) and h = 1 (p[2], p[3])
-            const int g = m & 3;
-            uint32_t wd[2];
+        for (int j = 0; j < 8; ++j) o[j] = (wk[0][j] * xm + wk[1][j] * x0 + wk[2][j] * xp) + bk[j];
+        if constexpr (sizeof(S) == 4) {
+            float4* dst = reinterpret_cast<float4*>(e0 + rowi * C + m * 8);
+            dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+            dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+        } else {
+            uint32_t p[4];
 #pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const uint32_t lo = p[2 * hh], hi = p[2 * hh + 1];
-                wd[hh] = (((short)(lo & 0xffffu) > 0 ? 1u : 0u) << mbit(4 * g + 0)) |
-                         (((int)lo >= 0x10000 ? 1u : 0u) << mbit(4 * g + 1)) |
-                         (((short)(hi & 0xffffu) > 0 ? 1u : 0u) << mbit(4 * g + 2)) |
-                         (((int)hi >= 0x10000 ? 1u : 0u) << mbit(4 * g + 3));
-                wd[hh] |= (uint32_t)__shfl_xor((int)wd[hh], 1);
-                wd[hh] |= (uint32_t)__shfl_xor((int)wd[hh], 2);
-                // words (hh, Q) and (hh, Q ^ 1) in one dword (even Q low)
-                const uint32_t other = (uint32_t)__shfl_xor((int)wd[hh], 4);
-                wd[hh] = (m & 4) ? (other | (wd[hh] << 16)) : (wd[hh] | (other << 16));
+            for (int k = 0; k < 4; ++k) p[k] = pack2(o[2 * k], o[2 * k + 1]);
+            *reinterpret_cast<uint4*>(e0 + rowi * C + m * 8) = make_uint4(p[0], p[1], p[2], p[3]);
+            if (me0) {
+                // e_0 > 0 bits for block 0's backward (dilation 1: position = time) in the MFMA
+                // accumulator layout (common.h): channel 32 Q + 8 g + 4 h + j is element
+                // i = 4 g + j of word (h, Q), at bit mbit(i); this lane holds Q = m / 4, g = m % 4,
+                // h = 0 (p[0], p[1]) and h = 1 (p[2], p[3])
+                const int g = m & 3;
+                uint32_t wd[2];
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const uint32_t lo = p[2 * hh], hi = p[2 * hh + 1];
+                    wd[hh] = (((short)(lo & 0xffffu) > 0 ? 1u : 0u) << mbit(4 * g + 0)) |
+                             (((int)lo >= 0x10000 ? 1u : 0u) << mbit(4 * g + 1)) |
+                             (((short)(hi & 0xffffu) > 0 ? 1u : 0u) << mbit(4 * g + 2)) |
+                             (((int)hi >= 0x10000 ? 1u : 0u) << mbit(4 * g + 3));
+                    wd[hh] |= (uint32_t)__shfl_xor((int)wd[hh], 1);
+                    wd[hh] |= (uint32_t)__shfl_xor((int)wd[hh], 2);
+                    // words (hh, Q) and (hh, Q ^ 1) in one dword (even Q low)
+                    const uint32_t other = (uint32_t)__shfl_xor((int)wd[hh], 4);
+                    wd[hh] = (m & 4) ? (other | (wd[hh] << 16)) : (wd[hh] | (other << 16));
+                }
+                // dwords [h0: Q0|Q1, Q2|Q3, h1: Q0|Q1, Q2|Q3]: lane m = 0 holds Q0|Q1, lane 8 Q2|Q3
+                const uint32_t f0 = (uint32_t)__shfl_xor((int)wd[0], 8);
+                const uint32_t f1 = (uint32_t)__shfl_xor((int)wd[1], 8);
+                if (m == 0)
+                    *reinterpret_cast<uint4*>(me0 + rowi * 8) = make_uint4(wd[0], f0, wd[1], f1);
             }
-            // dwords [h0: Q0|Q1, Q2|Q3, h1: Q0|Q1, Q2|Q3]: lane m = 0 holds Q0|Q1, lane 8 Q2|Q3
-            const uint32_t f0 = (uint32_t)__shfl_xor((int)wd[0], 8);
-            const uint32_t f1 = (uint32_t)__shfl_xor((int)wd[1], 8);
-            if (m == 0)
-                *reinterpret_cast<uint4*>(me0 + rowi * 8) = make_uint4(wd[0], f0, wd[1], f1);
         }
     }
 }
@@ -390,8 +395,7 @@ void launch_block_bwd(const BwdArgs& a, hipStream_t s) {
 template <typename S>
 void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b0, int B, int T,
                           hipStream_t s, uint16_t* me0) {
-    const size_t n = (size_t)B * T * 16;
-    hipLaunchKernelGGL(k_startconv_fwd<S>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x,
+    hipLaunchKernelGGL(k_startconv_fwd<S>, dim3((unsigned)((size_t)B * T / SFR)), dim3(256), 0, s, x,
                        e0, w0, b0, B, T, me0);
 }
 template <typename S>
