@@ -241,14 +241,15 @@ def _bf16(a):
     return t.to(torch.float32).numpy().astype(np.float64)
 
 
-@pytest.mark.parametrize('tag', ['c1', 'trunc', 'ours', 'gatys'])
-def test_bf16_backward_linearized(tag, weights, dev):
+@pytest.mark.parametrize('tag,T', [('c1', 2048), ('trunc', 2048), ('ours', 2048), ('gatys', 2048),
+                                   ('ours', 16384)])
+def test_bf16_backward_linearized(tag, T, weights, dev):
     """The bf16 backward against the fp64 backward linearised at the GPU's own bf16 forward:
     its activations (read back exactly), the relu patterns they imply, the bf16-rounded block
     weights and the loss gradients of its own extracts.  What remains is the backward's own
     rounding (g_u, D and the chain are stored in bf16), so a wrong halo row, mask bit, tap or
-    direct-gradient add at any dilation shows up far above the bound."""
-    T = 2048
+    direct-gradient add at any dilation shows up far above the bound.  T = 16384 is the bench
+    size, where dilations 128 / 256 / 512 give the one-segment / 64 / 32-position layouts."""
     kw = CASES[tag]
     phi_c, phi_s = _targets(tag, T, weights)
     x = O.mu_law_numpy(synthetic_clips(1, T, 42)[0]) + np.random.default_rng(5).normal(0, 4, T)
