@@ -280,7 +280,7 @@ def test_bf16_backward_linearized(tag, T, weights, dev):
     assert e <= 1.5e-2, e
 
 
-@pytest.mark.parametrize('T', [512, 2048])
+@pytest.mark.parametrize('T', [512, 1024, 2048])
 def test_bf16_extracts_and_embeds(T, weights, dev):
     kw = dict(CASES['trunc'], cont_ids=[29, 31], style_ids=[0, 9, 30])
     x = O.mu_law_numpy(synthetic_clips(1, T, 42)[0]) + np.random.default_rng(3).normal(0, 4, T)
