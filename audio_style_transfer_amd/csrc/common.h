@@ -57,10 +57,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #endif
 
 // bf16 path (precision 1) tile geometry
-constexpr int TMB = 128;      // rows per encoder tile
-constexpr int XSB = 136;      // LDS row stride in bf16 (272 B: ds_read_b128 conflict-free)
-constexpr int GTB = 32;       // Gram: time rows per stage
-constexpr int GCB = 32;       // Gram: channels per workgroup
+constexpr int TMB = 128;      // positions per encoder tile (colwave.h)
 
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float((uint32_t)v << 16); }
 __device__ __forceinline__ float bflo(uint32_t v) { return __uint_as_float(v << 16); }
