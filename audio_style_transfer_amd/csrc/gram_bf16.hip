@@ -69,9 +69,13 @@ __global__ void __launch_bounds__(256) k_gram_fwd_bf16(GramArgs a) {
     // staging item: tensor su, 8-row time block stb, 8-channel octet so (octet fastest: 4
     // lanes cover one 64-B row segment)
     const int su = tid >> 3, stb = (tid >> 2) & 1, so = tid & 3;
-    const int uu = su < a.nu ? su : a.nu - 1;      // padding tensors: finite data, unused
-    const u16* src = act + (size_t)a.uid[uu] * a.tstride + (size_t)b * a.T * C + c0 + so * 8 +
-                     (size_t)stb * 8 * C;
+    // padding tensors (su >= nu) read a 16-B zero line (row stride 0) instead of re-fetching a
+    // real tensor: their Gram rows are unused
+    const bool real = su < a.nu;
+    const u16* src = real ? act + (size_t)a.uid[su] * a.tstride + (size_t)b * a.T * C + c0 + so * 8 +
+                            (size_t)stb * 8 * C
+                          : (const u16*)a.zero16;
+    const size_t rs = real ? C : 0;
     f32x16 acc[8];
 #pragma unroll
     for (int cc = 0; cc < 8; ++cc)
@@ -79,7 +83,7 @@ __global__ void __launch_bounds__(256) k_gram_fwd_bf16(GramArgs a) {
     uint4 in[8];
     auto load = [&](int t0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) in[k] = *reinterpret_cast<const uint4*>(src + (size_t)(t0 + k) * C);
+        for (int k = 0; k < 8; ++k) in[k] = *reinterpret_cast<const uint4*>(src + (size_t)(t0 + k) * rs);
     };
     load(tbeg);
     for (int t0 = tbeg; t0 < tbeg + tlen; t0 += GST) {
