@@ -16,7 +16,7 @@ MAX_TAPS = 32
 # Every symbol include/astyle.h declares (checked by tests/test_abi.py).
 EXPORTS = ('ast_create', 'ast_destroy', 'ast_workspace_bytes', 'ast_set_weight', 'ast_forward',
            'ast_get_extract', 'ast_embeds', 'ast_content_cols', 'ast_set_targets',
-           'ast_loss_grad', 'ast_adam_step', 'ast_adam_step_dev', 'ast_timing', 'ast_timing_read',
+           'ast_set_gamma', 'ast_loss_grad', 'ast_adam_step', 'ast_adam_step_dev', 'ast_timing', 'ast_timing_read',
            'ast_last_error')
 
 
@@ -26,7 +26,8 @@ class AstCfg(ctypes.Structure):
                 ('cnt_channels', ctypes.c_int),
                 ('n_style', ctypes.c_int), ('style_ids', ctypes.c_int * MAX_TAPS),
                 ('nb_channels', ctypes.c_int), ('gatys', ctypes.c_int),
-                ('precision', ctypes.c_int), ('lambd', ctypes.c_float)]
+                ('precision', ctypes.c_int), ('lambd', ctypes.c_float),
+                ('gamma', ctypes.c_float)]
 
 
 class AstError(RuntimeError):
@@ -57,6 +58,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         'ast_embeds': (i, [vp, vp, vp, vp, vp]),
         'ast_content_cols': (i, [vp]),
         'ast_set_targets': (i, [vp, vp, i, vp, i]),
+        'ast_set_gamma': (i, [vp, f]),
         'ast_loss_grad': (i, [vp, vp, vp, vp, vp]),
         'ast_adam_step': (i, [vp, vp, vp, vp, vp, i, f, f, f, f, vp]),
         'ast_adam_step_dev': (i, [vp, vp, vp, vp, vp, vp, f, f, f, f, vp]),

@@ -88,6 +88,9 @@ struct ast_ctx {
     float* bott = nullptr; float* gbott = nullptr;
     float* gpart = nullptr; float* smat = nullptr; float* spart = nullptr; float* cpart = nullptr;
     u16* smatb = nullptr;                   // bf16 S~ (Gatys, precision 1)
+    float2* stft_tw = nullptr;              // STFT regulariser: twiddles [1024]
+    float* stft_fpart = nullptr;            //   per-frame partial sums [B][nf]
+    float* stft_gfr = nullptr;              //   per-frame gradients [B][nf][1024]
     void* zero = nullptr;                   // 256 zero bytes
     size_t gpart_elems = 0, smat_elems = 0; // per context (mode-dependent)
     int ncpart = 0;
@@ -187,6 +190,8 @@ size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     n += (size_t)c->batch * C * 4;                          // spart
     n += 256;                                               // zero line
     n += (size_t)c->batch * x->occ.size() * (c->T / CROWS) * 4;
+    const int nf = stft_frames(c->T);
+    if (nf) n += 1024 * 8 + (size_t)c->batch * nf * (1 + 1024) * 4;   // STFT regulariser
     return n;
 }
 
@@ -366,6 +371,14 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     ALLOC(x->spart, (size_t)c.batch * C * 4);
     x->ncpart = (int)x->occ.size() * (c.T / CROWS);
     ALLOC(x->cpart, (size_t)c.batch * x->ncpart * 4);
+    if (const int nf = stft_frames(c.T)) {
+        ALLOC(x->stft_tw, 1024 * 8);
+        ALLOC(x->stft_fpart, (size_t)c.batch * nf * 4);
+        ALLOC(x->stft_gfr, (size_t)c.batch * nf * 1024 * 4);
+        launch_stft_twiddles(x->stft_tw, nullptr);
+        e = hipDeviceSynchronize();
+        if (e != hipSuccess) { ast_destroy(x); return fail(AST_E_HIP, hipGetErrorString(e)); }
+    }
 #undef ALLOC
     *out = x;
     return 0;
@@ -532,6 +545,12 @@ int ast_set_targets(ast_ctx* x, const float* phi_c, int phi_c_shared, const floa
     return 0;
 }
 
+int ast_set_gamma(ast_ctx* x, float gamma) {
+    if (!x) return fail(AST_E_ARG, "null argument");
+    x->cfg.gamma = gamma;
+    return 0;
+}
+
 int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* stream) {
     if (!x || !xd || !grad || !parts) return fail(AST_E_ARG, "null argument");
     if (!x->targets) return fail(AST_E_STATE, "ast_set_targets has not been called");
@@ -638,6 +657,10 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     else
         launch_finalize(parts, x->cpart, x->ncpart, 10.0f / ((float)c.T * (float)x->ncc), x->spart,
                         C, 1e3f / (float)(nb * x->L * x->L), c.lambd, c.batch, s);
+    // STFT regulariser (methods.py:121-125): TF evaluates it whatever gamma is, so parts[3]
+    // always holds it; its gradient enters grad only through gamma
+    launch_stft_reg(xd, x->stft_tw, x->stft_fpart, x->stft_gfr, grad, parts, c.gamma, c.batch,
+                    c.T, s);
     tmark(x, s);
     HIPCHK(hipGetLastError());
     if (x->timing && x->ev_used <= (int)x->ev.size()) x->timed_calls++;

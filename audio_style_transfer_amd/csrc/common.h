@@ -252,6 +252,12 @@ __host__ __device__ inline float pow_int(float b, int n) {
     return r;
 }
 
+// STFT regulariser (stft_reg.hip, methods.py:121-123): frames of 1024 / hop 512
+int stft_frames(int T);
+void launch_stft_twiddles(float2* tw, hipStream_t s);
+void launch_stft_reg(const float* x, const float2* tw, float* fpart, float* gfr, float* grad,
+                     float* parts, float gamma, int B, int T, hipStream_t s);
+
 void launch_adam(float* x, float* m, float* v, const float* g, size_t n, float lr, float b1,
                  float b2, float eps, float bc1, float bc2, hipStream_t s);
 void launch_adam_dev(float* x, float* m, float* v, const float* g, size_t n, int* step_dev,

@@ -32,7 +32,7 @@ def resolve_style_ids(stack=None, style_lyr_ids=None):
 class StyleEngine:
     def __init__(self, batch: int, T: int, cont_ids: Sequence[int], style_ids: Sequence[int],
                  cnt_channels: int = 128, nb_channels: int = 128, gatys: bool = False,
-                 lambd: float = 100.0, precision: str = 'fp32',
+                 lambd: float = 100.0, gamma: float = 0.0, precision: str = 'fp32',
                  device: Optional[torch.device] = None, weights=None, weight_seed: int = 0):
         self.lib = _lib.load()
         if device is None:
@@ -47,6 +47,7 @@ class StyleEngine:
         self.nb_channels = int(nb_channels)
         self.cnt_channels = int(cnt_channels)
         self.lambd = float(lambd)
+        self.gamma = float(gamma)
         cfg = _lib.AstCfg()
         cfg.batch, cfg.T = self.batch, self.T
         cfg.n_cont = len(self.cont_ids)
@@ -60,6 +61,7 @@ class StyleEngine:
         cfg.gatys = int(self.gatys)
         cfg.precision = PRECISIONS[precision]
         cfg.lambd = self.lambd
+        cfg.gamma = self.gamma
         self.precision = precision
         self._cfg = cfg
         h = ctypes.c_void_p()
@@ -150,9 +152,16 @@ class StyleEngine:
         _lib.check(self.lib.ast_set_targets(self.h, self._ptr(phi_c), int(c_shared),
                                             self._ptr(phi_s), int(s_shared)))
 
+    def set_gamma(self, gamma: float) -> None:
+        """The STFT regulariser weight (--gamma, methods.py:125)."""
+        _lib.check(self.lib.ast_set_gamma(self.h, float(gamma)))
+        self.gamma = float(gamma)
+
     def loss_grad(self, x: torch.Tensor, grad: Optional[torch.Tensor] = None,
                   parts: Optional[torch.Tensor] = None):
-        """Returns (parts [B, 4] = (total, content, style, reg=0), grad [B, T])."""
+        """Returns (parts [B, 4] = (total, content, style, reg), grad [B, T]).  reg is the STFT
+        regulariser (methods.py:121-123), evaluated whatever gamma is, as TF does; total and
+        grad include gamma * reg."""
         if self._targets is None:
             raise _lib.AstError('set_targets() first')
         if grad is None:

@@ -35,27 +35,6 @@ def load_weights(path):
     return None
 
 
-def stft_regularizer(x: torch.Tensor):
-    """methods.py:121-123: mean(abs(Re S) + abs(Im S)), S = stft(inv_mu_law(x), 1024, 512)
-    (periodic Hann, no padding), utils.abs/sign/inv_mu_law semantics (utils.py:92-104).
-    x: [B, T] (mu-law units) -> (value [B], d value / d x [B, T]) via autograd on the GPU."""
-    x = x.detach().requires_grad_(True)
-
-    def abs_tf(v):
-        return torch.clamp(v, min=1e-12) + torch.clamp(-v, min=0.0)
-
-    o = (x + 0.5) * 2.0 / 256.0
-    sgn = torch.where(o.abs() <= 1e-12, torch.zeros_like(o), o) / abs_tf(o)
-    a = sgn / 255.0 * (256.0 ** abs_tf(o) - 1)
-    a = torch.where(x == 0, x, a)
-    S = torch.stft(a, n_fft=1024, hop_length=512, win_length=1024,
-                   window=torch.hann_window(1024, periodic=True, dtype=x.dtype, device=x.device),
-                   center=False, return_complex=True)
-    reg = (abs_tf(S.real) + abs_tf(S.imag)).mean(dim=(-2, -1))
-    g, = torch.autograd.grad(reg.sum(), x)
-    return reg.detach(), g
-
-
 class GatysNet(object):
     """methods.py:19-216, on one GPU; ``batch`` > 1 optimises independent clips together."""
 
@@ -123,6 +102,7 @@ class GatysNet(object):
         self.engine = eng
         eng.set_targets(torch.as_tensor(phi_c, dtype=torch.float32),
                         torch.as_tensor(phi_s, dtype=torch.float32))
+        eng.set_gamma(gamma)                                              # methods.py:121-125
         T = self.batch_size
         x = np.zeros(T) + 1e-6 if x0 is None else np.asarray(x0, dtype=np.float64)  # methods.py:49-54
         xd = torch.empty(1, T, device=self.device)
@@ -131,14 +111,9 @@ class GatysNet(object):
 
         def fg(v):
             xd.copy_(torch.from_numpy(v.astype(np.float32)).view(1, T))
-            parts, grad = eng.loss_grad(xd)
-            reg = 0.0
-            if gamma != 0.0:
-                r, gr = stft_regularizer(xd)
-                grad = grad + gamma * gr
-                reg = float(r[0])
+            parts, grad = eng.loss_grad(xd)                               # incl. gamma * reg
             p = parts[0].cpu().numpy().astype(np.float64)
-            loss = float(p[0]) + gamma * reg
+            loss, reg = float(p[0]), float(p[3])
             history.append((loss, float(p[1]), float(p[2]), reg))
             if not state['i'] % 5:                                       # methods.py:152-155
                 log('Ep {0:}/{1:}-it {2:}({3:})-tlapse {4:.4f}s-loss{5:.4f}-{6:.4f}-{7:.4f}-{8:.4f}'.format(

@@ -17,6 +17,7 @@
  *                                (methods.py:113-119, 207-213)
  *   ast_loss_grad             <- one ScipyOptimizerInterface evaluation: sess.run([loss, grad])
  *                                of define_loss + tf.gradients w.r.t. x (methods.py:113-137,167)
+ *   ast_set_gamma             <- the --gamma constant of define_loss (methods.py:125)
  *   ast_adam_step             <- (new) fused optimiser update on the audio buffer; the
  *                                reference's optimiser is host L-BFGS-B (methods.py:133-137)
  *
@@ -58,6 +59,7 @@ typedef struct ast_cfg {
     int gatys;                       /* --gatys                      (methods.py:68-71) */
     int precision;                   /* 0 = fp32 storage + fp32 MFMA; 1 = bf16 storage + bf16 MFMA */
     float lambd;                     /* --lambd                      (methods.py:125) */
+    float gamma;                     /* --gamma, STFT regulariser    (methods.py:121-125) */
 } ast_cfg;
 
 /* Context lifetime. */
@@ -83,9 +85,14 @@ int ast_content_cols(ast_ctx* ctx);  /* n_cont_cols of emb_c */
 int ast_set_targets(ast_ctx* ctx, const float* phi_c_dev, int phi_c_shared,
                     const float* phi_s_dev, int phi_s_shared);
 
-/* One loss+grad evaluation of every clip: grad_dev [batch, T] (d loss / d x, gamma term
- * excluded), parts_dev [batch, 4] = (content + lambd*style, content, style, 0). */
+/* One loss+grad evaluation of every clip: grad_dev [batch, T] = d loss / d x, parts_dev
+ * [batch, 4] = (content + lambd*style + gamma*reg, content, style, reg).  reg is the STFT
+ * regulariser of methods.py:121-123 (0 when T < 1024: no full frame); like TF it is evaluated
+ * whatever gamma is, and enters the gradient only through gamma. */
 int ast_loss_grad(ast_ctx* ctx, const float* x_dev, float* grad_dev, float* parts_dev, void* stream);
+
+/* Change gamma (methods.py:125) without rebuilding the context. */
+int ast_set_gamma(ast_ctx* ctx, float gamma);
 
 /* Fused Adam on the audio buffer: m, v, x updated in place from grad_dev. step >= 1. */
 int ast_adam_step(ast_ctx* ctx, float* x_dev, float* m_dev, float* v_dev, const float* grad_dev,

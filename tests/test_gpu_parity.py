@@ -72,7 +72,7 @@ def test_loss_grad_matches_oracle(tag, weights, golden, dev):
     parts = parts.cpu().numpy()[0]
     grad = grad.cpu().numpy()[0]
     ref_parts = golden[tag + '_parts']
-    for k in range(3):
+    for k in range(4):      # parts[3]: the STFT regulariser, evaluated at gamma = 0 as TF does
         assert abs(parts[k] - ref_parts[k]) <= 1e-4 * abs(ref_parts[k]) + 1e-7, (k, parts, ref_parts)
     e = rel(grad, golden[tag + '_grad'])
     print('%s grad rel-L2 %.3g parts %s vs %s' % (tag, e, parts, ref_parts))

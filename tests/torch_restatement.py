@@ -68,3 +68,15 @@ def loss_fn(x, W, *, cont_ids, style_ids, phi_c, phi_s, lambd=100.0, gamma=0.0, 
     reg = torch.mean(_abs_tf(S.real) + _abs_tf(S.imag))
     total = content + lambd * style + gamma * reg
     return total, content, style, reg
+
+
+def stft_reg(x):
+    """The regulariser alone (methods.py:121-123) for x [B, T] -> (value [B], d value / d x)
+    by torch.stft + autograd."""
+    x = torch.as_tensor(x).detach().clone().requires_grad_(True)
+    S = torch.stft(_inv_mu_law_tf(x), n_fft=1024, hop_length=512, win_length=1024,
+                   window=torch.hann_window(1024, periodic=True, dtype=x.dtype),
+                   center=False, return_complex=True)
+    reg = (_abs_tf(S.real) + _abs_tf(S.imag)).mean(dim=(-2, -1))
+    g, = torch.autograd.grad(reg.sum(), x)
+    return reg.detach(), g
