@@ -16,7 +16,9 @@ MAX_TAPS = 32
 # Every symbol include/astyle.h declares (checked by tests/test_abi.py).
 EXPORTS = ('ast_create', 'ast_destroy', 'ast_workspace_bytes', 'ast_set_weight', 'ast_forward',
            'ast_get_extract', 'ast_embeds', 'ast_content_cols', 'ast_set_targets',
-           'ast_set_gamma', 'ast_loss_grad', 'ast_adam_step', 'ast_adam_step_dev', 'ast_timing', 'ast_timing_read',
+           'ast_set_gamma', 'ast_loss_grad', 'ast_adam_step', 'ast_adam_step_dev',
+           'ast_lbfgs_workspace_bytes', 'ast_lbfgs_begin', 'ast_lbfgs_step', 'ast_lbfgs_state',
+           'ast_timing', 'ast_timing_read',
            'ast_last_error')
 
 
@@ -62,6 +64,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         'ast_loss_grad': (i, [vp, vp, vp, vp, vp]),
         'ast_adam_step': (i, [vp, vp, vp, vp, vp, i, f, f, f, f, vp]),
         'ast_adam_step_dev': (i, [vp, vp, vp, vp, vp, vp, f, f, f, f, vp]),
+        'ast_lbfgs_workspace_bytes': (i, [vp, i, ctypes.POINTER(sz)]),
+        'ast_lbfgs_begin': (i, [vp, vp, vp, vp, vp, i, i, i, ctypes.c_double, ctypes.c_double, vp]),
+        'ast_lbfgs_step': (i, [vp, vp, vp, vp, vp, vp]),
+        'ast_lbfgs_state': (i, [vp, vp, vp, vp, vp]),
         'ast_timing': (i, [vp, i]),
         'ast_timing_read': (i, [vp, fp, i]),
         'ast_last_error': (ctypes.c_char_p, []),

@@ -91,6 +91,7 @@ struct ast_ctx {
     float2* stft_tw = nullptr;              // STFT regulariser: twiddles [1024]
     float* stft_fpart = nullptr;            //   per-frame partial sums [B][nf]
     float* stft_gfr = nullptr;              //   per-frame gradients [B][nf][1024]
+    int lb_m = 0;                           // L-BFGS-B history size of the last ast_lbfgs_begin
     void* zero = nullptr;                   // 256 zero bytes
     size_t gpart_elems = 0, smat_elems = 0; // per context (mode-dependent)
     int ncpart = 0;
@@ -681,6 +682,44 @@ int ast_adam_step_dev(ast_ctx* x, float* xd, float* m, float* v, const float* gr
                       float lr, float b1, float b2, float eps, void* stream) {
     if (!x || !xd || !m || !v || !grad || !step_dev) return fail(AST_E_ARG, "bad argument");
     launch_adam_dev(xd, m, v, grad, (size_t)x->cfg.batch * x->cfg.T, step_dev, lr, b1, b2, eps, S(stream));
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int ast_lbfgs_workspace_bytes(ast_ctx* x, int m, size_t* out) {
+    if (!x || !out) return fail(AST_E_ARG, "null argument");
+    if (m < 1 || m > 32) return fail(AST_E_ARG, "L-BFGS-B history m must be in 1..32");
+    *out = lbfgs_workspace_bytes(x->cfg.batch, x->cfg.T, m);
+    return 0;
+}
+
+int ast_lbfgs_begin(ast_ctx* x, void* ws, float* xd, const double* x0, const int* active, int m,
+                    int maxiter, int maxls, double ftol, double gtol, void* stream) {
+    if (!x || !ws || !xd) return fail(AST_E_ARG, "null argument");
+    if (m < 1 || m > 32) return fail(AST_E_ARG, "L-BFGS-B history m must be in 1..32");
+    if (maxiter < 1 || maxls < 1) return fail(AST_E_ARG, "maxiter and maxls must be >= 1");
+    if (!x0 && x->lb_m != m)
+        return fail(AST_E_STATE, "continuing needs a workspace started with the same m (pass x0)");
+    x->lb_m = m;
+    launch_lbfgs_begin(ws, xd, x0, active, x->cfg.batch, x->cfg.T, m, maxiter, maxls, ftol, gtol,
+                       S(stream));
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int ast_lbfgs_step(ast_ctx* x, void* ws, float* xd, const float* grad, const float* parts,
+                   void* stream) {
+    if (!x || !ws || !xd || !grad || !parts) return fail(AST_E_ARG, "null argument");
+    if (!x->lb_m) return fail(AST_E_STATE, "ast_lbfgs_begin has not been called");
+    launch_lbfgs_step(ws, xd, grad, parts, x->cfg.batch, x->cfg.T, x->lb_m, S(stream));
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int ast_lbfgs_state(ast_ctx* x, const void* ws, int* info, double* x64, void* stream) {
+    if (!x || !ws || !info) return fail(AST_E_ARG, "null argument");
+    if (!x->lb_m) return fail(AST_E_STATE, "ast_lbfgs_begin has not been called");
+    launch_lbfgs_state(ws, info, x64, x->cfg.batch, x->cfg.T, x->lb_m, S(stream));
     HIPCHK(hipGetLastError());
     return 0;
 }

@@ -258,6 +258,15 @@ void launch_stft_twiddles(float2* tw, hipStream_t s);
 void launch_stft_reg(const float* x, const float2* tw, float* fpart, float* gfr, float* grad,
                      float* parts, float gamma, int B, int T, hipStream_t s);
 
+// batched device L-BFGS-B (lbfgs.hip, methods.py:132-137)
+size_t lbfgs_workspace_bytes(int B, int T, int m);
+void launch_lbfgs_begin(void* ws, float* x, const double* x0, const int* active, int B, int T,
+                        int m, int maxiter, int maxls, double tol, double pgtol, hipStream_t s);
+void launch_lbfgs_step(void* ws, float* x, const float* grad, const float* parts, int B, int T,
+                       int m, hipStream_t s);
+void launch_lbfgs_state(const void* ws, int* info, double* x64, int B, int T, int m,
+                        hipStream_t s);
+
 void launch_adam(float* x, float* m, float* v, const float* g, size_t n, float lr, float b1,
                  float b2, float eps, float bc1, float bc2, hipStream_t s);
 void launch_adam_dev(float* x, float* m, float* v, const float* g, size_t n, int* step_dev,

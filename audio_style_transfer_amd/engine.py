@@ -238,3 +238,93 @@ class AdamLoop:
         else:
             self._eager()
         return self.parts
+
+
+class LbfgsLoop:
+    """The reference's optimiser on the device: one scipy L-BFGS-B ``minimize`` per clip
+    (methods.py:132-137; no bounds, history ``m``, ``maxiter`` / ``maxls`` / ``ftol`` / ``gtol``
+    as scipy's options), every clip advancing by one loss+grad evaluation per step
+    (ast_loss_grad + ast_lbfgs_step, optionally replayed from a captured HIP graph).  ``x``
+    [B, T] fp32 is the buffer the loss reads; the float64 iterate lives in the workspace."""
+
+    FTOL = 2.220446049250313e-09      # scipy minimize(method='L-BFGS-B') defaults
+    GTOL = 1e-5
+
+    def __init__(self, eng: StyleEngine, m: int = 10, maxiter: int = 100, maxls: int = 20,
+                 ftol: float = FTOL, gtol: float = GTOL, graph: bool = False):
+        self.eng = eng
+        dev = eng.device
+        nb = ctypes.c_size_t()
+        _lib.check(eng.lib.ast_lbfgs_workspace_bytes(eng.h, int(m), ctypes.byref(nb)))
+        self.ws = torch.zeros(nb.value, dtype=torch.uint8, device=dev)
+        self.x = torch.zeros(eng.batch, eng.T, device=dev)
+        self.grad = torch.empty_like(self.x)
+        self.parts = torch.zeros(eng.batch, 4, device=dev)
+        self.info = torch.zeros(eng.batch, 4, dtype=torch.int32, device=dev)
+        self.opts = (int(m), int(maxiter), int(maxls), float(ftol), float(gtol))
+        self.started = False
+        self.graph = None
+        if graph:
+            # capture records the pair without executing it; state lives in ws, so a replay
+            # is the same as an eager step whatever begin() set up
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._eager()
+            self.graph = g
+
+    def _p(self, t):
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+    def _eager(self):
+        eng = self.eng
+        eng.loss_grad(self.x, self.grad, self.parts)
+        _lib.check(eng.lib.ast_lbfgs_step(eng.h, self._p(self.ws), self._p(self.x),
+                                          self._p(self.grad), self._p(self.parts), eng._stream()))
+
+    def begin(self, x0: Optional[torch.Tensor] = None, active: Optional[torch.Tensor] = None):
+        """Start a minimize call per (active) clip from x0 [B, T] (float64), or from each clip's
+        current point (the next epoch, methods.py:164-167)."""
+        eng = self.eng
+        if x0 is None and not self.started:
+            raise _lib.AstError('the first begin() needs x0')
+        if x0 is not None:
+            x0 = x0.to(eng.device, torch.float64).contiguous()
+            assert x0.shape == (eng.batch, eng.T)
+        if active is not None:
+            active = active.to(eng.device, torch.int32).contiguous()
+        self._x0 = x0
+        m, maxiter, maxls, ftol, gtol = self.opts
+        _lib.check(eng.lib.ast_lbfgs_begin(eng.h, self._p(self.ws), self._p(self.x), self._p(x0),
+                                           self._p(active), m, maxiter, maxls,
+                                           ctypes.c_double(ftol), ctypes.c_double(gtol),
+                                           eng._stream()))
+        self.started = True
+
+    def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._eager()
+
+    def state(self, with_x: bool = False):
+        """(info [B, 4] int numpy = phase, iterations, evaluations, reason; x float64 [B, T] or
+        None)."""
+        x64 = torch.empty(self.eng.batch, self.eng.T, dtype=torch.float64,
+                          device=self.eng.device) if with_x else None
+        _lib.check(self.eng.lib.ast_lbfgs_state(self.eng.h, self._p(self.ws), self._p(self.info),
+                                                self._p(x64), self.eng._stream()))
+        return self.info.cpu().numpy(), x64
+
+    def minimize(self, x0: Optional[torch.Tensor] = None, active=None, check_every: int = 4,
+                 max_steps: int = 100000):
+        """Run until every clip's minimize call has returned; returns the final info."""
+        self.begin(x0, active)
+        steps = 0
+        while steps < max_steps:
+            for _ in range(check_every):
+                self.step()
+            steps += check_every
+            info, _ = self.state()
+            if not info[:, 0].any():
+                return info
+        raise _lib.AstError('L-BFGS-B did not finish within %d steps' % max_steps)

@@ -4,7 +4,7 @@ Same argparse surface (methods.py:243-269), same output layout (utils.gt_s_path 
 ori.wav, style.wav, ep-N.wav, gram/spectrogram PNGs), same optimisation protocol: per epoch one
 scipy L-BFGS-B minimize(maxiter=100) whose every function evaluation is one ast_loss_grad
 (ScipyOptimizerInterface, methods.py:132-137,167), early stop when an epoch used < 50
-evaluations (methods.py:180).  Additions: --optimizer adam (fused device Adam, many clips),
+evaluations (methods.py:180).  Additions: --optimizer device (the same L-BFGS-B on the GPU),
 --precision bf16, --weights (npz of TF-named encoder variables).
 
 The TF checkpoint itself cannot be read here (no TF): --ckpt_path is
@@ -42,7 +42,8 @@ class GatysNet(object):
                  checkpoint_path='./nsynth/model/wavenet-ckpt/model.ckpt-200000',
                  logdir='./log', figdir='./data/fig', stack=0, batch_size=16384, sr=16000,
                  cont_lyr_ids=[29], nb_channels=128, cnt_channels=128, gatys=False,
-                 style_lyr_ids=None, precision='fp32', device=None, weights=None, plots=True):
+                 style_lyr_ids=None, precision='fp32', device=None, weights=None, plots=True,
+                 optimizer='scipy'):
         self.logdir = logdir
         self.savepath = savepath
         self.checkpoint_path = checkpoint_path
@@ -56,6 +57,7 @@ class GatysNet(object):
         self.precision = precision
         self.device = device or torch.device('cuda', torch.cuda.current_device())
         self.plots = plots
+        self.optimizer = optimizer
         if weights is None:
             weights = load_weights(checkpoint_path)
             if weights is None:
@@ -95,8 +97,10 @@ class GatysNet(object):
             utils.show_gram(phi, figdir=self.figdir, gatys=self.gatys)
         return phi
 
-    def l_bfgs(self, phi_c, phi_s, epochs, lambd, gamma, x0=None, log=print):
-        """methods.py:140-181 with scipy L-BFGS-B driving ast_loss_grad."""
+    def l_bfgs(self, phi_c, phi_s, epochs, lambd, gamma, x0=None, log=print, optimizer='scipy'):
+        """methods.py:140-181 with scipy L-BFGS-B driving ast_loss_grad (``optimizer='scipy'``,
+        one host round trip per evaluation, as the reference), or the same L-BFGS-B run on the
+        device (``'device'``: ast_lbfgs_*, no round trip; progress is logged per epoch)."""
         from scipy.optimize import minimize
         eng = self.build(self.batch_size, lambd=lambd) if lambd != self.engine.lambd else self.engine
         self.engine = eng
@@ -122,10 +126,23 @@ class GatysNet(object):
             state['i'] += 1
             return loss, grad[0].double().cpu().numpy()
 
+        loop = None
+        if optimizer == 'device':
+            from .engine import LbfgsLoop
+            loop = LbfgsLoop(eng, maxiter=100)
         for ep in range(epochs):
             state['ep'], state['i'] = ep, 0
-            res = minimize(fg, x, jac=True, method='L-BFGS-B', options={'maxiter': 100})
-            x = res.x
+            if loop is None:
+                res = minimize(fg, x, jac=True, method='L-BFGS-B', options={'maxiter': 100})
+                x = res.x
+            else:
+                info = loop.minimize(torch.tensor(x[None], dtype=torch.float64) if ep == 0 else None)
+                x = loop.state(with_x=True)[1][0].cpu().numpy()
+                state['i'] = int(info[0, 2])
+                p = loop.parts[0].cpu().numpy().astype(np.float64)
+                history.append((float(p[0]), float(p[1]), float(p[2]), float(p[3])))
+                log('Ep {0:}/{1:}-it {2:}-tlapse {3:.4f}s-loss{4:.4f}-{5:.4f}-{6:.4f}-{7:.4f}'.format(
+                    ep + 1, epochs, state['i'], time.time() - state['since'], *p))
             state['i_'] = state['i']
             audio = utils.inv_mu_law_numpy(x[None])[0, self.late:-self.late]
             sp = os.path.join(self.savepath, 'ep-{}.wav'.format(ep))
@@ -155,7 +172,8 @@ class GatysNet(object):
         phi = self.get_embeds(aud, is_content=False)
         phi = phi + phi_t - phi_s
         phi = phi / np.sqrt(np.maximum(np.sum(phi * phi, axis=(1, 2), keepdims=True), 1e-12))
-        x = self.l_bfgs(phi_c, phi, epochs=epochs, lambd=lambd, gamma=gamma)
+        x = self.l_bfgs(phi_c, phi, epochs=epochs, lambd=lambd, gamma=gamma,
+                        optimizer=self.optimizer)
         return utils.inv_mu_law_numpy(x[None])[0]
 
 
@@ -169,7 +187,7 @@ def get_fpath(fn, args):
     return os.path.join(args.dir, fn) + '.wav'
 
 
-EXTRA_FLAGS = ('precision', 'weights', 'no_plots')
+EXTRA_FLAGS = ('precision', 'weights', 'no_plots', 'optimizer')
 
 
 def piece_work(args):
@@ -181,7 +199,8 @@ def piece_work(args):
     weights = load_weights(args.weights) if args.weights else None
     test = GatysNet(savepath, args.ckpt_path, logdir, figdir, args.stack, args.batch_size, args.sr,
                     args.cont_lyrs, args.channels, args.cnt_channels, args.gatys, args.style_lyrs,
-                    precision=args.precision, weights=weights, plots=not args.no_plots)
+                    precision=args.precision, weights=weights, plots=not args.no_plots,
+                    optimizer=args.optimizer)
     return test.run(content, content, style, epochs=args.epochs, lambd=args.lambd,
                     gamma=args.gamma, start=args.start)
 
@@ -214,6 +233,9 @@ def make_parser():
                         help='fp32: reference numerics; bf16: bf16 storage + bf16 MFMA')
     parser.add_argument('--weights', default=None, help='npz of TF-named encoder weights')
     parser.add_argument('--no_plots', action='store_true', help='skip the Gram PNGs')
+    parser.add_argument('--optimizer', default='scipy', choices=['scipy', 'device'],
+                        help='scipy: host L-BFGS-B per evaluation (reference); device: the same '
+                             'L-BFGS-B on the GPU (ast_lbfgs_*)')
     return parser
 
 

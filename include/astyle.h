@@ -18,6 +18,8 @@
  *   ast_loss_grad             <- one ScipyOptimizerInterface evaluation: sess.run([loss, grad])
  *                                of define_loss + tf.gradients w.r.t. x (methods.py:113-137,167)
  *   ast_set_gamma             <- the --gamma constant of define_loss (methods.py:125)
+ *   ast_lbfgs_*               <- scipy L-BFGS-B under ScipyOptimizerInterface.minimize
+ *                                (methods.py:132-137,164-181), per clip on the device
  *   ast_adam_step             <- (new) fused optimiser update on the audio buffer; the
  *                                reference's optimiser is host L-BFGS-B (methods.py:133-137)
  *
@@ -101,6 +103,27 @@ int ast_adam_step(ast_ctx* ctx, float* x_dev, float* m_dev, float* v_dev, const 
  * captured hipGraph of {ast_loss_grad, ast_adam_step_dev} replays as consecutive steps. */
 int ast_adam_step_dev(ast_ctx* ctx, float* x_dev, float* m_dev, float* v_dev, const float* grad_dev,
                       int* step_dev, float lr, float beta1, float beta2, float eps, void* stream);
+
+/* Device-resident batched L-BFGS-B: one scipy.optimize.minimize(method='L-BFGS-B') call per
+ * clip (no bounds; history m, maxiter, maxls, ftol = factr*eps, gtol = pgtol as scipy's
+ * options), all clips advancing together, one loss+grad evaluation per step:
+ *   ast_lbfgs_begin(x0)                       x_dev <- fp32(x0): the first point to evaluate
+ *   repeat { ast_loss_grad(x_dev -> grad, parts); ast_lbfgs_step(grad, parts) -> next x_dev }
+ *   until every clip's phase (ast_lbfgs_state) is 0
+ * ws_dev: caller-owned device workspace of ast_lbfgs_workspace_bytes.  x0_dev [batch, T]
+ * float64 (NULL: continue from each clip's current point, the next epoch of methods.py:164);
+ * active_dev [batch] int (NULL = all) selects the clips that run.  info_dev [batch, 4] =
+ * (phase, iterations, evaluations, reason: 0 running, 1 maxiter, 2 pgtol, 3 rel. reduction
+ * of f, 4 abnormal line search); x64_dev [batch, T] (may be NULL) the current float64 point.
+ * begin/step allocate nothing, so the step pair is hipGraph-capturable. */
+int ast_lbfgs_workspace_bytes(ast_ctx* ctx, int m, size_t* out_bytes);
+int ast_lbfgs_begin(ast_ctx* ctx, void* ws_dev, float* x_dev, const double* x0_dev,
+                    const int* active_dev, int m, int maxiter, int maxls, double ftol,
+                    double gtol, void* stream);
+int ast_lbfgs_step(ast_ctx* ctx, void* ws_dev, float* x_dev, const float* grad_dev,
+                   const float* parts_dev, void* stream);
+int ast_lbfgs_state(ast_ctx* ctx, const void* ws_dev, int* info_dev, double* x64_dev,
+                    void* stream);
 
 /* Per-kernel-family device timing (HIP events on the call's stream).  enable!=0 starts
  * recording; ast_timing_read fills out[0..n) with milliseconds summed since enable for
