@@ -263,14 +263,8 @@ class LbfgsLoop:
         self.info = torch.zeros(eng.batch, 4, dtype=torch.int32, device=dev)
         self.opts = (int(m), int(maxiter), int(maxls), float(ftol), float(gtol))
         self.started = False
+        self.use_graph = bool(graph)
         self.graph = None
-        if graph:
-            # capture records the pair without executing it; state lives in ws, so a replay
-            # is the same as an eager step whatever begin() set up
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._eager()
-            self.graph = g
 
     def _p(self, t):
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
@@ -301,7 +295,14 @@ class LbfgsLoop:
         self.started = True
 
     def step(self):
-        if self.graph is not None:
+        if self.use_graph:
+            if self.graph is None:
+                # captured at the first step after begin(): capture records the pair without
+                # executing it, and the state lives in ws, so every replay is an eager step
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._eager()
+                self.graph = g
             self.graph.replay()
         else:
             self._eager()

@@ -42,6 +42,8 @@ def parse():
                          'fp32: fp32 storage + fp32 MFMA (parity mode)')
     ap.add_argument('--fp32-steps', type=int, default=2,
                     help='also time the fp32 parity mode for this many steps (N=1 only; 0 = off)')
+    ap.add_argument('--lbfgs-steps', type=int, default=5,
+                    help='side measurement: steps of the device L-BFGS-B mode (0: skip)')
     ap.add_argument('--gatys', action='store_true',
                     help='configs[4]: Gatys [L,128,128] Gram instead of the channel-wise one')
     ap.add_argument('--lr', type=float, default=2.0)
@@ -165,6 +167,52 @@ def run(args, precision, steps, warmup, ws, rank, dev, graph):
     return el, tm, first_loss, last_loss
 
 
+def run_lbfgs(args, steps, dev):
+    """Side measurement (rank 0, N=1): the reference's optimiser, scipy's L-BFGS-B restated on
+    the device (ast_lbfgs_*), over the same 256-clip workload.  A step is one evaluation of every
+    clip (ast_loss_grad) + one ast_lbfgs_step, replayed from a HIP graph; the L-BFGS-B kernel's
+    own time comes from HIP events around eager launches on the engine's stream."""
+    import ctypes
+    from audio_style_transfer_amd.engine import StyleEngine, LbfgsLoop
+    from audio_style_transfer_amd.shard import clip_range
+    B, T = args.clips, args.T
+    eng = StyleEngine(B, T, [29], list(range(30)), precision=args.precision, device=dev,
+                      lambd=100.0, gatys=args.gatys)
+    x = make_problem(eng, clip_range(B, 1, 0), T, dev)
+    loop = LbfgsLoop(eng, maxiter=100, graph=bool(args.graph))
+    loop.begin(x.double())
+    for _ in range(2):
+        loop.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loop.step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    s = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ms = 0.0
+    for _ in range(3):
+        eng.loss_grad(loop.x, loop.grad, loop.parts)
+        e0.record(s)
+        eng.lib.ast_lbfgs_step(eng.h, ctypes.c_void_p(loop.ws.data_ptr()),
+                               ctypes.c_void_p(loop.x.data_ptr()),
+                               ctypes.c_void_p(loop.grad.data_ptr()),
+                               ctypes.c_void_p(loop.parts.data_ptr()), eng._stream())
+        e1.record(s)
+        torch.cuda.synchronize()
+        ms += e0.elapsed_time(e1) / 3
+    info, _ = loop.state()
+    del loop, x
+    eng.close()
+    torch.cuda.empty_cache()
+    return {'value': B * steps / 256.0 / el, 'unit': 'iters/s', 'steps': steps,
+            'lbfgs_step_ms': ms, 'clips_running': int((info[:, 0] != 0).sum()),
+            'note': 'device L-BFGS-B (scipy semantics: m 10, dcsrch line search, maxiter 100) '
+                    'instead of Adam, same workload; one iter = one loss+grad evaluation of every '
+                    'clip + the L-BFGS-B update'}
+
+
 def main():
     args = parse()
     ws, rank, local = dist_setup()
@@ -180,6 +228,9 @@ def main():
                      'steps': args.fp32_steps,
                      'note': 'same workload with fp32 storage + fp32 MFMA (parity mode: grad '
                              'within 2e-3 rel-L2 of the fp64 oracle)'}
+    lbfgs_side = None
+    if args.lbfgs_steps > 0 and ws == 1:
+        lbfgs_side = run_lbfgs(args, args.lbfgs_steps, dev)
     if rank != 0:
         barrier(ws)
         return
@@ -249,6 +300,8 @@ def main():
     }
     if fp32_side:
         out['fp32_mode'] = fp32_side
+    if lbfgs_side:
+        out['lbfgs_mode'] = lbfgs_side
     if ws == 1 and args.cpu_baseline_seconds > 0:
         out['cpu_baseline'] = cpu_baseline(T, args.cpu_baseline_seconds)
     print(json.dumps(out), flush=True)
