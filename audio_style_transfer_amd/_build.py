@@ -10,8 +10,9 @@ from concurrent.futures import ThreadPoolExecutor
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, 'csrc')
 LIB = os.path.join(PKG, 'libastyle.so')
-SOURCES = ['encoder.hip', 'block_fwd_bf16.hip', 'block_bwd_bf16.hip', 'gram.hip',
-           'gram_bf16.hip', 'gram_gatys.hip', 'stft_reg.hip', 'lbfgs.hip', 'api.hip']
+SOURCES = ['encoder.hip', 'block_fwd_bf16.hip', 'block_bwd_bf16.hip', 'block_fwd_split.hip',
+           'block_bwd_split.hip', 'gram.hip', 'gram_bf16.hip', 'gram_gatys.hip', 'stft_reg.hip',
+           'lbfgs.hip', 'api.hip']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall',
          '-Wno-unused-function', '-munsafe-fp-atomics']
@@ -20,7 +21,8 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall',
 # unrolled tile loops exceed the default pragma-unroll size limit (a partly unrolled loop would
 # index the register-resident weight arrays dynamically and demote them to scratch)
 _CW = ['-mllvm', '-amdgpu-mfma-vgpr-form=1', '-mllvm', '-pragma-unroll-threshold=1000000']
-EXTRA = {'block_fwd_bf16.hip': _CW, 'block_bwd_bf16.hip': _CW}
+EXTRA = {'block_fwd_bf16.hip': _CW, 'block_bwd_bf16.hip': _CW, 'block_fwd_split.hip': _CW,
+         'block_bwd_split.hip': _CW}
 
 
 def _stale() -> bool:

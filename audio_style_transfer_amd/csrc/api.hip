@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <cmath>
 
 #include "../../include/astyle.h"
 #include "common.h"
@@ -52,6 +53,28 @@ constexpr size_t W_TOTAL = BB_OFF + 16;
 // WRBFB [4 q][8 kb][64][8], element e = W_r[32 q + m][16 kb + 8 h + e]
 constexpr size_t WFB = 0, WRFB = 3 * C * C, WBFB = 4 * C * C, WRBFB = 7 * C * C, BLKB_SZ = 8 * C * C;
 inline int kperm(int s, int h, int e) { return 32 * (s >> 1) + 16 * (s & 1) + (e & 3) + 8 * (e >> 2) + 4 * h; }
+// split-fp16 fragments (precision 2), uint4 (8 fp16) units per block: WDF [4][3][8][2][64],
+// WRF [4][8][2][64], WRB [4][8][2][64], WDB [4][3][8][2][64] (common.h, FwdArgsS / BwdArgsS)
+constexpr size_t SWDF = 0, SWRF = 4 * 3 * 8 * 2 * 64, SWRB = SWRF + 4 * 8 * 2 * 64,
+                 SWDB = SWRB + 4 * 8 * 2 * 64, SBLK = SWDB + 4 * 3 * 8 * 2 * 64;
+
+// power-of-two exponent k that puts max |w| in [2^13, 2^14) (fp16 range, splitwave.h)
+int weight_exp(const float* w, size_t n) {
+    float mx = 0.f;
+    for (size_t i = 0; i < n; ++i) mx = std::max(mx, std::fabs(w[i]));
+    if (!(mx > 0.f) || !std::isfinite(mx)) return 0;
+    int e = 0;
+    (void)std::frexp(mx, &e);
+    return 14 - e;
+}
+// fp16 halves of w 2^k (round to nearest): hi, lo = fp16(w 2^k - hi)
+void split_half(float w, int k, uint16_t& hi, uint16_t& lo) {
+    const float v = std::ldexp(w, k);
+    const _Float16 h = (_Float16)v;
+    const _Float16 l = (_Float16)(v - (float)h);
+    memcpy(&hi, &h, 2);
+    memcpy(&lo, &l, 2);
+}
 
 uint16_t host_bf16(float f) {   // round to nearest even
     uint32_t u;
@@ -80,7 +103,12 @@ struct ast_ctx {
     // device memory
     float* wts = nullptr;
     u16* wtsb = nullptr;                    // bf16 weight copies (precision 1)
+    uint4* wtss = nullptr;                  // split-fp16 weight fragments (precision 2)
+    int kd[NBLK_MAX] = {}, kr[NBLK_MAX] = {};   // their exponents
     bool bf = false;                        // precision 1: bf16 activations/gradients
+    bool split = false;                     // precision 2: fp32 storage, split-fp16 block GEMMs
+    unsigned* gmax_e = nullptr;             // [nblk + 1][B] max |e_l| per clip (precision 2)
+    unsigned* gmax_g = nullptr;             // [nblk + 1][B] max |d loss / d e_l| per clip
     size_t esz = 4;                         // bytes per stored element
     void* act = nullptr; size_t tstride = 0;
     uint32_t* mu = nullptr; uint32_t* me = nullptr;
@@ -118,7 +146,8 @@ int plan(const ast_cfg* c, ast_ctx* x) {
         return fail(AST_E_ARG, "need 1..32 content and style taps");
     if (c->cnt_channels < 1 || c->nb_channels < 1)
         return fail(AST_E_ARG, "cnt_channels / nb_channels must be >= 1");
-    if (c->precision != 0 && c->precision != 1) return fail(AST_E_ARG, "precision must be 0 (fp32) or 1 (bf16)");
+    if (c->precision < 0 || c->precision > 2)
+        return fail(AST_E_ARG, "precision must be 0 (fp32), 1 (bf16) or 2 (split: fp32 storage, split-fp16 MFMA)");
     int top = 0;
     x->need_bott = false;
     x->ncc = 0;
@@ -178,6 +207,7 @@ size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     const size_t es = c->precision == 1 ? 2 : 4;
     size_t n = 0;
     n += W_TOTAL * 4 + (size_t)NBLK_MAX * BLKB_SZ * 2;
+    if (c->precision == 2) n += (size_t)NBLK_MAX * SBLK * 16 + 2 * (size_t)(NBLK_MAX + 1) * c->batch * 4;
     n += (size_t)(x->nblk + 1) * BTC * es;                  // act
     n += 2 * (size_t)x->nblk * c->batch * c->T * 16;        // mu, me
     n += 2 * BTC * es;                                      // chain
@@ -215,7 +245,11 @@ void* tens(ast_ctx* x, int t) { return (char*)x->act + (size_t)t * x->tstride * 
 
 int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
     const ast_cfg& c = x->cfg;
-    if (x->bf) launch_startconv_fwd((const float*)xd, (u16*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s, (uint16_t*)x->me);
+    if (x->split) {
+        HIPCHK(hipMemsetAsync(x->gmax_e, 0, (size_t)(NBLK_MAX + 1) * c.batch * 4, s));
+        launch_startconv_fwd((const float*)xd, (float*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s,
+                             (uint16_t*)x->me, x->gmax_e);
+    } else if (x->bf) launch_startconv_fwd((const float*)xd, (u16*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s, (uint16_t*)x->me);
     else launch_startconv_fwd((const float*)xd, (float*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s);
     if (mark) tmark(x, s);
     for (int l = 0; l < x->nblk; ++l) {
@@ -223,7 +257,21 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
         const int d = 1 << (l % 10);
         uint32_t* mu = x->mu + (size_t)l * c.batch * c.T * 4;
         uint32_t* me = x->me + (size_t)l * c.batch * c.T * 4;
-        if (x->bf) {
+        if (x->split) {
+            FwdArgsS a;
+            const uint4* ws = x->wtss + (size_t)l * SBLK;
+            a.ein = (const float*)tens(x, l); a.eout = (float*)tens(x, l + 1);
+            a.wdf = ws + SWDF; a.wrf = ws + SWRF; a.bd = w + BD; a.br = w + BR;
+            a.mu = (uint16_t*)mu;
+            a.me_next = l + 1 < x->nblk ? (uint16_t*)(me + (size_t)c.batch * c.T * 4) : nullptr;
+            a.gmax_in = (const float*)(x->gmax_e + (size_t)l * c.batch);
+            a.gmax_out = x->gmax_e + (size_t)(l + 1) * c.batch;
+            a.zero = (const float*)x->zero;
+            a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
+            a.dn_log2 = (l + 1) % 10; a.nn = c.T >> a.dn_log2;
+            a.kd = x->kd[l]; a.kr = x->kr[l];
+            launch_block_fwd_s(a, s);
+        } else if (x->bf) {
             FwdArgsC a;
             a.stamps = g_stamps;
             u16* wb = blkwb(x, l);
@@ -348,7 +396,14 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     void* p;
 #define ALLOC(dst, bytes) do { if ((rc = dalloc(x, &p, (bytes)))) { ast_destroy(x); return rc; } dst = (decltype(dst))p; } while (0)
     x->bf = c.precision == 1;
+    x->split = c.precision == 2;
     x->esz = x->bf ? 2 : 4;
+    if (x->split) {
+        ALLOC(x->wtss, (size_t)NBLK_MAX * SBLK * 16);
+        (void)hipMemset(x->wtss, 0, (size_t)NBLK_MAX * SBLK * 16);
+        ALLOC(x->gmax_e, (size_t)(NBLK_MAX + 1) * c.batch * 4);
+        ALLOC(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4);
+    }
     ALLOC(x->wts, W_TOTAL * 4);
     (void)hipMemset(x->wts, 0, W_TOTAL * 4);
     ALLOC(x->wtsb, (size_t)NBLK_MAX * BLKB_SZ * 2);
@@ -439,6 +494,27 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
             u16* dst = x->wtsb + (size_t)(l - 1) * BLKB_SZ;
             HIPCHK(hipMemcpy(dst + WFB, hf.data(), 3 * C * C * 2, hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(dst + WBFB, hg.data(), 3 * C * C * 2, hipMemcpyHostToDevice));
+            if (x->split) {
+                // forward: element (w, tap, kb, hl, lane (m, h), e) = W_d[tap][16 kb + 8 h + e][32 w + m];
+                // backward: W_d[tap][32 w + m][16 kb + 8 h + e]
+                const int k = weight_exp(host, 3 * C * C);
+                x->kd[l - 1] = k;
+                std::vector<uint16_t> f(3 * C * C * 2), g(3 * C * C * 2);
+                for (int w = 0; w < 4; ++w)
+                    for (int tp = 0; tp < 3; ++tp)
+                        for (int kb = 0; kb < 8; ++kb)
+                            for (int ln = 0; ln < 64; ++ln)
+                                for (int e = 0; e < 8; ++e) {
+                                    const int m = ln & 31, hh = ln >> 5;
+                                    const int kk = 16 * kb + 8 * hh + e, mm = 32 * w + m;
+                                    const size_t o = ((((size_t)(w * 3 + tp) * 8 + kb) * 2) * 64 + ln) * 8 + e;
+                                    split_half(host[(size_t)tp * C * C + kk * C + mm], k, f[o], f[o + 64 * 8]);
+                                    split_half(host[(size_t)tp * C * C + mm * C + kk], k, g[o], g[o + 64 * 8]);
+                                }
+                uint4* ds = x->wtss + (size_t)(l - 1) * SBLK;
+                HIPCHK(hipMemcpy(ds + SWDF, f.data(), f.size() * 2, hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(ds + SWDB, g.data(), g.size() * 2, hipMemcpyHostToDevice));
+            }
             return 0;
         }
         if (!strcmp(tail, "biases")) { if ((rc = need(C))) return rc; return put(base + BD, host, C); }
@@ -467,6 +543,26 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
             u16* dst = x->wtsb + (size_t)(l - 1) * BLKB_SZ;
             HIPCHK(hipMemcpy(dst + WRFB, hf.data(), C * C * 2, hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(dst + WRBFB, hg.data(), C * C * 2, hipMemcpyHostToDevice));
+            if (x->split) {
+                // forward: element (w, kb, hl, lane (m, h), e) = W_r[16 kb + 8 h + e][32 w + m];
+                // backward: W_r[32 w + m][16 kb + 8 h + e]
+                const int k = weight_exp(host, C * C);
+                x->kr[l - 1] = k;
+                std::vector<uint16_t> f(C * C * 2), g(C * C * 2);
+                for (int w = 0; w < 4; ++w)
+                    for (int kb = 0; kb < 8; ++kb)
+                        for (int ln = 0; ln < 64; ++ln)
+                            for (int e = 0; e < 8; ++e) {
+                                const int m = ln & 31, hh = ln >> 5;
+                                const int kk = 16 * kb + 8 * hh + e, mm = 32 * w + m;
+                                const size_t o = ((((size_t)w * 8 + kb) * 2) * 64 + ln) * 8 + e;
+                                split_half(host[(size_t)kk * C + mm], k, f[o], f[o + 64 * 8]);
+                                split_half(host[(size_t)mm * C + kk], k, g[o], g[o + 64 * 8]);
+                            }
+                uint4* ds = x->wtss + (size_t)(l - 1) * SBLK;
+                HIPCHK(hipMemcpy(ds + SWRF, f.data(), f.size() * 2, hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(ds + SWRB, g.data(), g.size() * 2, hipMemcpyHostToDevice));
+            }
             return 0;
         }
         if (!strcmp(tail, "biases")) { if ((rc = need(C))) return rc; return put(base + BR, host, C); }
@@ -617,6 +713,12 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     auto direct = [&](int t) -> const void* {   // D_t: direct loss gradient of tensor t (or null)
         return x->tensor_in_style[t] ? tens(x, t) : x->cg_buf[t];
     };
+    if (x->split) {
+        HIPCHK(hipMemsetAsync(x->gmax_g, 0, (size_t)(NBLK_MAX + 1) * c.batch * 4, s));
+        const void* top = direct(x->nblk);
+        if (!top) return fail(AST_E_STATE, "top block has no loss gradient");
+        launch_absmax((const float*)top, (size_t)c.T * C, c.batch, x->gmax_g + (size_t)x->nblk * c.batch, s);
+    }
     for (int l = x->nblk - 1; l >= 0; --l) {
         float* w = blkw(x, l);
         const int tin = l + 1;
@@ -625,7 +727,22 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
         const uint32_t* mu = x->mu + (size_t)l * c.batch * c.T * 4;
         const uint32_t* me = x->me + (size_t)l * c.batch * c.T * 4;
         const int d = 1 << (l % 10);
-        if (x->bf) {
+        if (x->split) {
+            // like the bf16 chain, the chain holds d loss / d e_l with D_l already added
+            BwdArgsS a;
+            const uint4* ws = x->wtss + (size_t)l * SBLK;
+            a.tin = (const float*)(gin ? gin : din);
+            a.dadd = l > 0 ? (const float*)direct(l) : nullptr;
+            a.gout = (float*)x->chain[l & 1];
+            a.wrb = ws + SWRB; a.wdb = ws + SWDB;
+            a.mu = (const uint16_t*)mu; a.me = (const uint16_t*)me;
+            a.gmax_in = (const float*)(x->gmax_g + (size_t)(l + 1) * c.batch);
+            a.gmax_out = x->gmax_g + (size_t)l * c.batch;
+            a.zero = (const float*)x->zero;
+            a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
+            a.kd = x->kd[l]; a.kr = x->kr[l];
+            launch_block_bwd_s(a, s);
+        } else if (x->bf) {
             // the bf16 chain holds d loss / d e_l with D_l already added (the kernel adds it)
             BwdArgsC a;
             a.stamps = g_stamps;

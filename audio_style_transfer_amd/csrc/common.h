@@ -153,6 +153,40 @@ struct BwdArgsC {
     int B, T, d, n;        // dilation, n = T / d
 };
 
+// split-fp16 block kernels (precision 2: block_fwd_split.hip, block_bwd_split.hip).  Weight
+// fragments are fp16 halves of W 2^k (k = kd / kr per block, host-chosen), 8 halves per lane:
+//   wdf [4 w][3 tap][8 kb][2 hl][64 lanes]: lane (m, h) element e = W_d[tap][16 kb + 8 h + e][32 w + m]
+//   wrf [4 w][8 kb][2 hl][64]:                                     W_r[16 kb + 8 h + e][32 w + m]
+//   wrb [4 w][8 kb][2 hl][64]:                                     W_r[32 w + m][16 kb + 8 h + e]
+//   wdb [4 w][3 tap][8 kb][2 hl][64]:                              W_d[tap][32 w + m][16 kb + 8 h + e]
+// gmax_*: per clip max |x| of a tensor as float bits (atomic max of the non-negative bit pattern).
+struct FwdArgsS {
+    const float* ein; float* eout;
+    const uint4* wdf; const uint4* wrf;
+    const float* bd; const float* br;
+    uint16_t* mu;          // [B*T][2 h][4 w] u > 0 bits, this layer's positions
+    uint16_t* me_next;     // [B*T][2][4] e_{l+1} > 0 bits, the next layer's positions (or null)
+    const float* gmax_in;  // [B] max |e_l|
+    unsigned* gmax_out;    // [B] max |e_{l+1}| (atomic)
+    const float* zero;     // >= 16 zero bytes
+    int B, T, d, n;        // dilation, n = T / d
+    int dn_log2, nn;       // next layer: log2 dilation, T / dilation
+    int kd, kr;            // weight exponents
+};
+
+struct BwdArgsS {
+    const float* tin;      // d loss / d e_{l+1} incl. its direct term
+    const float* dadd;     // D_l (or null)
+    float* gout;           // d loss / d e_l incl. D_l
+    const uint4* wrb; const uint4* wdb;
+    const uint16_t* mu; const uint16_t* me;
+    const float* gmax_in;  // [B] max |tot|
+    unsigned* gmax_out;    // [B] max |out| (atomic)
+    const float* zero;
+    int B, T, d, n;
+    int kd, kr;
+};
+
 struct GramArgs {
     const void* act; size_t tstride;       // tensor u lives at act + uid[u] * tstride elements
     void* actw;                             // same base, writable (bwd, in place)
@@ -211,7 +245,8 @@ struct ContentArgs {
 // launchers (encoder.hip / gram.hip / optim.hip)
 template <typename S>
 void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b0,
-                          int B, int T, hipStream_t s, uint16_t* me0 = nullptr);
+                          int B, int T, hipStream_t s, uint16_t* me0 = nullptr,
+                          unsigned* gmax = nullptr);
 template <typename S>
 void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T,
                           hipStream_t s);
@@ -219,6 +254,9 @@ void launch_block_fwd(const FwdArgs& a, hipStream_t s);
 void launch_block_bwd(const BwdArgs& a, hipStream_t s);
 void launch_block_fwd_c(const FwdArgsC& a, hipStream_t s);
 void launch_block_bwd_c(const BwdArgsC& a, hipStream_t s);
+void launch_block_fwd_s(const FwdArgsS& a, hipStream_t s);
+void launch_block_bwd_s(const BwdArgsS& a, hipStream_t s);
+void launch_absmax(const float* x, size_t per_clip, int B, unsigned* out, hipStream_t s);
 template <typename S>
 void launch_bottleneck_fwd(const S* e, float* y, const float* wb, const float* bb,
                            int B, int T, hipStream_t s);

@@ -225,12 +225,18 @@ __global__ void __launch_bounds__(256) k_block_bwd(BwdArgs a) {
 // ae_startconv (model.py:88-93): 1 -> 128 channels, K=3, d=1, input x/128 (model.py:82).
 // Thread per (row, 8 channels): 16-B bf16 (32-B fp32) stores, 16 lanes per row.
 constexpr int SFR = 256;   // rows per workgroup
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    return v;
+}
 template <typename S>
 __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__ x,
                                                        S* __restrict__ e0,
                                                        const float* __restrict__ w0,
                                                        const float* __restrict__ b0, int B,
-                                                       int T, uint16_t* __restrict__ me0) {
+                                                       int T, uint16_t* __restrict__ me0,
+                                                       unsigned* __restrict__ gmax) {
     // SFR rows per workgroup, 16 lanes per row; this lane's 8 channels' weights load once
     const int m = threadIdx.x & 15;
     float wk[3][8], bk[8];
@@ -239,6 +245,7 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
         wk[0][j] = w0[m * 8 + j]; wk[1][j] = w0[C + m * 8 + j]; wk[2][j] = w0[2 * C + m * 8 + j];
         bk[j] = b0[m * 8 + j];
     }
+    float amax = 0.f;
     for (int it = 0; it < SFR / 16; ++it) {
         const size_t rowi = (size_t)blockIdx.x * SFR + it * 16 + (threadIdx.x >> 4);
         const int t = (int)(rowi % T);
@@ -249,42 +256,59 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = (wk[0][j] * xm + wk[1][j] * x0 + wk[2][j] * xp) + bk[j];
+        // element j > 0 (the stored value: fp32, or its bf16 rounding)
+        bool pos[8];
         if constexpr (sizeof(S) == 4) {
             float4* dst = reinterpret_cast<float4*>(e0 + rowi * C + m * 8);
             dst[0] = make_float4(o[0], o[1], o[2], o[3]);
             dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pos[j] = o[j] > 0.f;
         } else {
             uint32_t p[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) p[k] = pack2(o[2 * k], o[2 * k + 1]);
             *reinterpret_cast<uint4*>(e0 + rowi * C + m * 8) = make_uint4(p[0], p[1], p[2], p[3]);
-            if (me0) {
-                // e_0 > 0 bits for block 0's backward (dilation 1: position = time) in the MFMA
-                // accumulator layout (common.h): channel 32 Q + 8 g + 4 h + j is element
-                // i = 4 g + j of word (h, Q), at bit mbit(i); this lane holds Q = m / 4, g = m % 4,
-                // h = 0 (p[0], p[1]) and h = 1 (p[2], p[3])
-                const int g = m & 3;
-                uint32_t wd[2];
 #pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const uint32_t lo = p[2 * hh], hi = p[2 * hh + 1];
-                    wd[hh] = (((short)(lo & 0xffffu) > 0 ? 1u : 0u) << mbit(4 * g + 0)) |
-                             (((int)lo >= 0x10000 ? 1u : 0u) << mbit(4 * g + 1)) |
-                             (((short)(hi & 0xffffu) > 0 ? 1u : 0u) << mbit(4 * g + 2)) |
-                             (((int)hi >= 0x10000 ? 1u : 0u) << mbit(4 * g + 3));
-                    wd[hh] |= (uint32_t)__shfl_xor((int)wd[hh], 1);
-                    wd[hh] |= (uint32_t)__shfl_xor((int)wd[hh], 2);
-                    // words (hh, Q) and (hh, Q ^ 1) in one dword (even Q low)
-                    const uint32_t other = (uint32_t)__shfl_xor((int)wd[hh], 4);
-                    wd[hh] = (m & 4) ? (other | (wd[hh] << 16)) : (wd[hh] | (other << 16));
-                }
-                // dwords [h0: Q0|Q1, Q2|Q3, h1: Q0|Q1, Q2|Q3]: lane m = 0 holds Q0|Q1, lane 8 Q2|Q3
-                const uint32_t f0 = (uint32_t)__shfl_xor((int)wd[0], 8);
-                const uint32_t f1 = (uint32_t)__shfl_xor((int)wd[1], 8);
-                if (m == 0)
-                    *reinterpret_cast<uint4*>(me0 + rowi * 8) = make_uint4(wd[0], f0, wd[1], f1);
+            for (int k = 0; k < 4; ++k) {
+                pos[2 * k] = (short)(p[k] & 0xffffu) > 0;
+                pos[2 * k + 1] = (int)p[k] >= 0x10000;
             }
         }
+        if (gmax) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(o[j]));
+        }
+        if (me0) {
+            // e_0 > 0 bits for block 0's backward (dilation 1: position = time) in the MFMA
+            // accumulator layout (common.h): channel 32 Q + 8 g + 4 h + j is element
+            // i = 4 g + j of word (h, Q), at bit mbit(i); this lane holds Q = m / 4, g = m % 4,
+            // h = 0 (elements 0..3) and h = 1 (elements 4..7)
+            const int g = m & 3;
+            uint32_t wd[2];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                wd[hh] = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) wd[hh] |= (pos[4 * hh + j] ? 1u : 0u) << mbit(4 * g + j);
+                wd[hh] |= (uint32_t)__shfl_xor((int)wd[hh], 1);
+                wd[hh] |= (uint32_t)__shfl_xor((int)wd[hh], 2);
+                // words (hh, Q) and (hh, Q ^ 1) in one dword (even Q low)
+                const uint32_t other = (uint32_t)__shfl_xor((int)wd[hh], 4);
+                wd[hh] = (m & 4) ? (other | (wd[hh] << 16)) : (wd[hh] | (other << 16));
+            }
+            // dwords [h0: Q0|Q1, Q2|Q3, h1: Q0|Q1, Q2|Q3]: lane m = 0 holds Q0|Q1, lane 8 Q2|Q3
+            const uint32_t f0 = (uint32_t)__shfl_xor((int)wd[0], 8);
+            const uint32_t f1 = (uint32_t)__shfl_xor((int)wd[1], 8);
+            if (m == 0)
+                *reinterpret_cast<uint4*>(me0 + rowi * 8) = make_uint4(wd[0], f0, wd[1], f1);
+        }
+    }
+    if (gmax) {
+        // max |e_0| of the workgroup's rows (one clip: T is a multiple of SFR) -> the clip's max
+        amax = wave_max_f(amax);
+        if ((threadIdx.x & 63) == 0)
+            atomicMax(gmax + (size_t)blockIdx.x * SFR / T, __float_as_uint(amax));
     }
 }
 
@@ -394,9 +418,9 @@ void launch_block_bwd(const BwdArgs& a, hipStream_t s) {
 }
 template <typename S>
 void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b0, int B, int T,
-                          hipStream_t s, uint16_t* me0) {
+                          hipStream_t s, uint16_t* me0, unsigned* gmax) {
     hipLaunchKernelGGL(k_startconv_fwd<S>, dim3((unsigned)((size_t)B * T / SFR)), dim3(256), 0, s, x,
-                       e0, w0, b0, B, T, me0);
+                       e0, w0, b0, B, T, me0, gmax);
 }
 template <typename S>
 void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T, hipStream_t s) {
@@ -420,8 +444,8 @@ void launch_bottleneck_bwd(const float* gy, S* ge, const float* wb, int accumula
 void launch_to_f32(const u16* src, float* dst, size_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_to_f32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, n);
 }
-template void launch_startconv_fwd<float>(const float*, float*, const float*, const float*, int, int, hipStream_t, uint16_t*);
-template void launch_startconv_fwd<u16>(const float*, u16*, const float*, const float*, int, int, hipStream_t, uint16_t*);
+template void launch_startconv_fwd<float>(const float*, float*, const float*, const float*, int, int, hipStream_t, uint16_t*, unsigned*);
+template void launch_startconv_fwd<u16>(const float*, u16*, const float*, const float*, int, int, hipStream_t, uint16_t*, unsigned*);
 template void launch_startconv_bwd<float>(const float*, float*, const float*, int, int, hipStream_t);
 template void launch_startconv_bwd<u16>(const u16*, float*, const float*, int, int, hipStream_t);
 template void launch_bottleneck_fwd<float>(const float*, float*, const float*, const float*, int, int, hipStream_t);

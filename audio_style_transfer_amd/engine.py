@@ -16,7 +16,7 @@ import torch
 from . import _lib
 from .weights import synthetic_weights
 
-PRECISIONS = {'fp32': 0, 'bf16': 1}
+PRECISIONS = {'fp32': 0, 'bf16': 1, 'split': 2}
 
 
 def resolve_style_ids(stack=None, style_lyr_ids=None):

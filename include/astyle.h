@@ -59,7 +59,10 @@ typedef struct ast_cfg {
     int style_ids[AST_MAX_TAPS];     /* extract ids 0..30 */
     int nb_channels;                 /* --channels                   (methods.py:75,258) */
     int gatys;                       /* --gatys                      (methods.py:68-71) */
-    int precision;                   /* 0 = fp32 storage + fp32 MFMA; 1 = bf16 storage + bf16 MFMA */
+    int precision;                   /* 0 = fp32 storage + fp32 MFMA; 1 = bf16 storage + bf16 MFMA;
+                                        2 = fp32 storage, encoder GEMMs on split-fp16 MFMA (each
+                                        fp32 operand as two fp16 halves, 3 products, fp32
+                                        accumulation), Gram on bf16 MFMA */
     float lambd;                     /* --lambd                      (methods.py:125) */
     float gamma;                     /* --gamma, STFT regulariser    (methods.py:121-125) */
 } ast_cfg;
