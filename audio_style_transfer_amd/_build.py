@@ -11,7 +11,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, 'csrc')
 LIB = os.path.join(PKG, 'libastyle.so')
 SOURCES = ['encoder.hip', 'block_fwd_bf16.hip', 'block_bwd_bf16.hip', 'block_fwd_split.hip',
-           'block_bwd_split.hip', 'gram.hip', 'gram_bf16.hip', 'gram_gatys.hip', 'stft_reg.hip',
+           'block_bwd_split.hip', 'gram.hip', 'gram_bf16.hip', 'gram_split.hip', 'gram_gatys.hip', 'stft_reg.hip',
            'lbfgs.hip', 'api.hip']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall',

@@ -183,18 +183,15 @@ int plan(const ast_cfg* c, ast_ctx* x) {
     // every dilation used must divide T (masked.py:134)
     const int maxd = x->nblk >= 10 ? 512 : (1 << (x->nblk - 1));
     if (c->T % maxd) return fail(AST_E_ARG, "T must be a multiple of the largest dilation");
+    // Gram time chunks: a fixed length per T, whatever the batch, so a clip's partial sums (and
+    // so its result, bit for bit) do not depend on how many clips share the context
     int nch = 1;
     if (c->gatys) {
-        // Gatys Gram time chunks: >= ~2048 workgroups over (clip, tensor, chunk), chunk a
-        // multiple of 64 rows
-        const int target = std::max(1, 2048 / (c->batch * x->nu));
-        while (nch * 2 <= target && (c->T / 64) % (nch * 2) == 0) nch *= 2;
+        nch = std::max(1, c->T / 4096);        // multiples of 64 rows
         x->gpart_elems = (size_t)c->batch * nch * x->nu * C * C;
         x->smat_elems = (size_t)c->batch * x->nu * C * C;
     } else {
-        // channel-wise Gram time chunks: ~4096 workgroups, chunk a multiple of GT
-        const int target = std::max(1, 4096 / (8 * c->batch));
-        while (nch * 2 <= target && (c->T / GT) % (nch * 2) == 0) nch *= 2;
+        nch = std::max(1, c->T / 1024);        // multiples of the stage lengths (16 / 32 rows)
         x->gpart_elems = (size_t)c->batch * nch * C * 1024;
         x->smat_elems = (size_t)c->batch * C * 1024;
     }
@@ -259,6 +256,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
         uint32_t* me = x->me + (size_t)l * c.batch * c.T * 4;
         if (x->split) {
             FwdArgsS a;
+            a.stamps = g_stamps;
             const uint4* ws = x->wtss + (size_t)l * SBLK;
             a.ein = (const float*)tens(x, l); a.eout = (float*)tens(x, l + 1);
             a.wdf = ws + SWDF; a.wrf = ws + SWRF; a.bd = w + BD; a.br = w + BR;
@@ -303,10 +301,14 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
 }
 
 void launch_gram_fwd_any(ast_ctx* x, const GramArgs& g, hipStream_t s) {
-    if (x->bf) launch_gram_fwd_bf16(g, s); else launch_gram_fwd(g, s);
+    if (x->bf) launch_gram_fwd_bf16(g, s);
+    else if (x->split) launch_gram_fwd_s(g, s);
+    else launch_gram_fwd(g, s);
 }
 void launch_gram_bwd_any(ast_ctx* x, const GramArgs& g, hipStream_t s) {
-    if (x->bf) launch_gram_bwd_bf16(g, s); else launch_gram_bwd(g, s);
+    if (x->bf) launch_gram_bwd_bf16(g, s);
+    else if (x->split) launch_gram_bwd_s(g, s);
+    else launch_gram_bwd(g, s);
 }
 
 GramArgs gram_args(ast_ctx* x) {
@@ -730,6 +732,7 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
         if (x->split) {
             // like the bf16 chain, the chain holds d loss / d e_l with D_l already added
             BwdArgsS a;
+            a.stamps = g_stamps;
             const uint4* ws = x->wtss + (size_t)l * SBLK;
             a.tin = (const float*)(gin ? gin : din);
             a.dadd = l > 0 ? (const float*)direct(l) : nullptr;

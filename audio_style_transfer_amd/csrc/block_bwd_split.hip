@@ -131,6 +131,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     const int Lh = r == 1 ? TMS + 1 : 0;
 
     int it = 0;
+    STAMP_DECL
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
         const int cur = it & 1;
         const Tile cu = tile_of(tile);
@@ -145,9 +146,11 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         }
         issue_tile(tile + (int)gridDim.x < ntiles ? tile + (int)gridDim.x : ntiles - 1, cur ^ 1);
 
+        STAMP(6)
         const int m_t = scale_exp(sload(a.gmax_in + cu.b));
         convert_rows<false>(&XF[cur][0], XS, ly.nrows, exp2i(m_t), w, lane);
         lds_barrier();     // B2
+        STAMP(7)
 
         bool ok0[2] = {true, true}, ok2[2] = {true, true};
         if (MASKED) {
@@ -236,6 +239,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         // this wave's D_l rows have landed (younger: the next tile's 9 row groups + 1 mask group)
         if (HAS_D) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
         lds_barrier();     // B4: g_u image complete (and every wave's D_l rows)
+        STAMP(8)
 
         // ---- step 2: g_a = sum_k W_d[k] g_u(p - k + 1) ----
         {
@@ -266,6 +270,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             }
         }
 
+        STAMP(9)
         // ---- epilogue: out = tot + [e_l > 0] g_a + D_l ----
         {
             float omax = 0.f;
@@ -296,7 +301,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             omax = wave_max(omax);
             if (lane == 0) atomicMax(a.gmax_out + cu.b, __float_as_uint(omax));
         }
+        STAMP(10)
     }
+    STAMP_FLUSH(a.stamps)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 

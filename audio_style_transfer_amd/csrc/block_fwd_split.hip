@@ -91,6 +91,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     };
 
     int it = 0, prevb = 0;
+    STAMP_DECL
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
         const int cur = it & 1;
         const Tile cu = tile_of(tile);
@@ -103,9 +104,11 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         if (it) store_me(prevb);
         issue_rows(tile + (int)gridDim.x < ntiles ? tile + (int)gridDim.x : ntiles - 1, cur ^ 1);
 
+        STAMP(0)
         const int m_e = scale_exp(sload(a.gmax_in + cu.b));
         convert_rows<true>(&XF[cur][0], XS, ly.nrows, exp2i(m_e), w, lane);
         lds_barrier();     // B2: split image complete
+        STAMP(1)
 
         bool ok0[2] = {true, true}, ok2[2] = {true, true};
         if (MASKED) {
@@ -151,6 +154,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             }
         }
 
+        STAMP(2)
         // ---- epilogue 1: u, u > 0 words, v = relu(u) ----
         {
             const float inv1 = exp2i(-(m_e + a.kd));
@@ -196,6 +200,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             *reinterpret_cast<uint4*>(a.mu + ((size_t)cu.b * a.T + cu.p0 + 16 * w + lane) * 8) =
                 *reinterpret_cast<const uint4*>(&MBU[(16 * w + lane) * 8]);
         lds_barrier();     // B4: v image complete
+        STAMP(3)
 
         // ---- GEMM 2: y = W_r^T v ----
 #pragma unroll
@@ -223,6 +228,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             }
         }
 
+        STAMP(4)
         // ---- epilogue 2: e_{l+1} = e_l + y + b_r ----
         {
             const float inv2 = exp2i(-(m_v + a.kr));
@@ -254,7 +260,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             if (lane == 0) atomicMax(a.gmax_out + cu.b, __float_as_uint(emax));
         }
         prevb = cu.b;
+        STAMP(5)
     }
+    STAMP_FLUSH(a.stamps)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (it) store_me(prevb);

@@ -161,6 +161,7 @@ struct BwdArgsC {
 //   wdb [4 w][3 tap][8 kb][2 hl][64]:                              W_d[tap][32 w + m][16 kb + 8 h + e]
 // gmax_*: per clip max |x| of a tensor as float bits (atomic max of the non-negative bit pattern).
 struct FwdArgsS {
+    unsigned long long* stamps;            // diagnostic builds (-DASTYLE_STAMPS) only
     const float* ein; float* eout;
     const uint4* wdf; const uint4* wrf;
     const float* bd; const float* br;
@@ -175,6 +176,7 @@ struct FwdArgsS {
 };
 
 struct BwdArgsS {
+    unsigned long long* stamps;            // diagnostic builds (-DASTYLE_STAMPS) only
     const float* tin;      // d loss / d e_{l+1} incl. its direct term
     const float* dadd;     // D_l (or null)
     float* gout;           // d loss / d e_l incl. D_l
@@ -267,6 +269,8 @@ void launch_to_f32(const u16* src, float* dst, size_t n, hipStream_t s);
 void launch_gram_fwd_bf16(const GramArgs& a, hipStream_t s);
 void launch_gram_bwd_bf16(const GramArgs& a, hipStream_t s);
 void launch_gram_fwd(const GramArgs& a, hipStream_t s);
+void launch_gram_fwd_s(const GramArgs& a, hipStream_t s);   // precision 2: bf16 MFMA, fp32 E
+void launch_gram_bwd_s(const GramArgs& a, hipStream_t s);
 void launch_gram_bwd(const GramArgs& a, hipStream_t s);
 void launch_style_ours(const StyleArgs& a, hipStream_t s);
 void launch_gatys_fwd(const GatysArgs& a, bool bf16, hipStream_t s);

@@ -1,0 +1,243 @@
+// Channel-wise ("ours") Gram forward/backward on bf16 MFMA over fp32 activations (precision 2),
+// methods.py:62-76.  The activations stay fp32 in HBM.  Each Gram operand is carried as two
+// bf16 terms, x ~ xh + xl (xh = bf16(x), xl = bf16(x - xh)), and every product as
+// xh yh + xh yl + xl yh on v_mfma_*_bf16 with fp32 accumulation: the Gram is HBM-bound (10
+// flop/B), so the three products cost no time, and they keep the gradient at fp32-class error
+// where one bf16 product does not (an L = 2 style Gram: 1.8e-3 rel-L2 from the bf16 backward
+// alone, tools/precision_emulate.py).  D leaves in fp32.
+//
+// Per (clip, time chunk, 32-channel group) workgroup, 8 waves x 4 channels, stages of 16 time
+// rows; the next stage's global loads are in flight while a stage computes:
+//   fwd  G_c = E_c E_c^T      v_mfma_f32_32x32x16_bf16, A = B fragments (lane (u, h):
+//                             E_u[t0 + 8 h .. + 8][c]) from an LDS image [c][u][hi t | lo t]
+//   bwd  D_c = S~_c E_c       v_mfma_f32_16x16x32_bf16 (A = S~_c halves in registers, B: lane
+//                             (t, kq): E_{8 kq .. + 8}[t][c]) from LDS images [c][t][u] (hi, lo);
+//                             D goes back through an fp32 image [u][t][c] in two halves of 16
+//                             tensors and leaves as whole 128-B lines, in place over E (+ the
+//                             content grad)
+// Loads and stores move whole 128-B lines (8 lanes x 16 B per row).
+#include "common.h"
+
+namespace ast {
+namespace {
+
+constexpr int GCS = 32;       // channels per workgroup
+constexpr int GSS = 16;       // time rows per stage
+constexpr int GWT = 512;      // threads per workgroup (8 waves x 4 channels)
+constexpr int FRS = 40;       // fwd image [c][u][hi 16 | lo 16 | pad 8] row stride (bf16): 80 B
+constexpr int BRS = 40;       // bwd images [c][t][u] row stride (bf16): 80 B
+constexpr int ORS = 36;       // bwd output image [u][t][c] row stride (floats): 144 B
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+    return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+}
+
+__device__ __forceinline__ void decode(const GramArgs& a, int& b, int& ch, int& c0) {
+    constexpr int ncg = C / GCS;
+    const int nwg = a.B * a.nchunk * ncg;
+    int work = xcd_remap(blockIdx.x, nwg);   // the 4 channel groups of a chunk share one XCD
+    const int cgi = work % ncg; work /= ncg;
+    ch = work % a.nchunk;
+    b = work / a.nchunk;
+    c0 = cgi * GCS;
+}
+
+// bf16 pair (x0, x1) and the pair of their remainders
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+    hi = pack2(x0, x1);
+    lo = pack2(x0 - bflo(hi), x1 - bfhi(hi));
+}
+// 8 values (one channel of 8 loaded float4) -> hi / lo 16-B fragment runs
+template <int J>
+__device__ __forceinline__ void split8(const float4 (&v)[8], uint4& hi, uint4& lo) {
+    auto e = [&](int k) { return J == 0 ? v[k].x : J == 1 ? v[k].y : J == 2 ? v[k].z : v[k].w; };
+    uint32_t h[4], l[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) split2(e(2 * p), e(2 * p + 1), h[p], l[p]);
+    hi = make_uint4(h[0], h[1], h[2], h[3]);
+    lo = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
+// forward.  Staging: thread (w, l) loads tensor u = 8 (w & 3) + (l & 7), channel quad l >> 3,
+// rows t0 + 8 (w >> 2) + k (k = 0..7): one load instruction covers 8 whole lines.
+__global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
+    __shared__ __attribute__((aligned(16))) u16 I[GCS * 32 * FRS];   // [c][u][hi t | lo t]
+    int b, ch, c0;
+    decode(a, b, ch, c0);
+    const int tlen = a.T / a.nchunk, tbeg = ch * tlen;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int su = 8 * (w & 3) + (lane & 7), sq = lane >> 3, tb = w >> 2;
+    const bool real = su < a.nu;
+    const float* src = real ? (const float*)a.act + (size_t)a.uid[su] * a.tstride +
+                              (size_t)b * a.T * C + c0 + 4 * sq + (size_t)8 * tb * C
+                            : (const float*)a.zero16;
+    const size_t rs = real ? C : 0;
+    f32x16 acc[4];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[cc][i] = 0.f;
+    float4 v[8];
+    auto load = [&](int t0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
+    };
+    load(tbeg);
+    for (int t0 = tbeg; t0 < tbeg + tlen; t0 += GSS) {
+        uint4 fh[4], fl[4];          // channel 4 sq + j: 8 consecutive rows, hi / lo
+        split8<0>(v, fh[0], fl[0]);
+        split8<1>(v, fh[1], fl[1]);
+        split8<2>(v, fh[2], fl[2]);
+        split8<3>(v, fh[3], fl[3]);
+        if (t0 + GSS < tbeg + tlen) load(t0 + GSS);     // next stage in flight during this one
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            u16* row = &I[((4 * sq + j) * 32 + su) * FRS + 8 * tb];
+            *reinterpret_cast<uint4*>(row) = fh[j];
+            *reinterpret_cast<uint4*>(row + 16) = fl[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const u16* row = &I[((4 * w + cc) * 32 + r) * FRS + 8 * h];
+            const uint4 xh = *reinterpret_cast<const uint4*>(row);
+            const uint4 xl = *reinterpret_cast<const uint4*>(row + 16);
+            acc[cc] = mfma_bf16(xh, xh, acc[cc]);
+            acc[cc] = mfma_bf16(xh, xl, acc[cc]);
+            acc[cc] = mfma_bf16(xl, xh, acc[cc]);
+        }
+    }
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+        float* dst = a.gpart + (((size_t)b * a.nchunk + ch) * C + c0 + 4 * w + cc) * 1024;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dst[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = acc[cc][i];
+    }
+}
+
+// backward.  Staging: thread (w, l) loads tensors 8 (w & 3) + k (k = 0..7), channel quad
+// l >> 3, row t0 + 8 (w >> 2) + (l & 7).  Output: 16 tensors at a time through O; padding
+// tensors (u >= nu) are neither read nor written.
+__global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
+    __shared__ __attribute__((aligned(16))) u16 IH[GCS * GSS * BRS];       // [c][t][u] hi
+    __shared__ __attribute__((aligned(16))) u16 IL[GCS * GSS * BRS];       // [c][t][u] lo
+    __shared__ __attribute__((aligned(16))) float O[16 * GSS * ORS];       // [u][t][c]
+    int b, ch, c0;
+    decode(a, b, ch, c0);
+    const int tlen = a.T / a.nchunk, tbeg = ch * tlen, tend = tbeg + tlen;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int i16 = lane & 15, kq = lane >> 4;
+    // A fragments (16x16x32): S~_c[u = 16 m + i16][u' = 8 kq .. + 8] as bf16 hi / lo; wave w
+    // owns channels 4 w .. 4 w + 3
+    uint4 sa[4][2][2];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const float* sm = a.smat + ((size_t)b * C + c0 + 4 * w + cc) * 1024 + (16 * m + i16) * 32 + 8 * kq;
+            const float4 p = *reinterpret_cast<const float4*>(sm);
+            const float4 q = *reinterpret_cast<const float4*>(sm + 4);
+            uint32_t h[4], l[4];
+            split2(p.x, p.y, h[0], l[0]);
+            split2(p.z, p.w, h[1], l[1]);
+            split2(q.x, q.y, h[2], l[2]);
+            split2(q.z, q.w, h[3], l[3]);
+            sa[cc][m][0] = make_uint4(h[0], h[1], h[2], h[3]);
+            sa[cc][m][1] = make_uint4(l[0], l[1], l[2], l[3]);
+        }
+    // staging loads: tensors 8 uo + k, quad sq, row st of the stage
+    const int uo = w & 3, sq = lane >> 3, st = 8 * (w >> 2) + (lane & 7);
+    const size_t rowoff = (size_t)b * a.T * C + c0 + 4 * sq;
+    const float* ld[8];
+    size_t lrs[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int u = 8 * uo + k;
+        ld[k] = u < a.nu ? (const float*)a.act + (size_t)a.uid[u] * a.tstride + rowoff : (const float*)a.zero16;
+        lrs[k] = u < a.nu ? C : 0;
+    }
+    float4 v[8];
+    auto load = [&](int t0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (size_t)(t0 + st) * lrs[k]);
+    };
+    load(tbeg);
+    for (int t0 = tbeg; t0 < tend; t0 += GSS) {
+        uint4 fh[4], fl[4];   // channel 4 sq + j: tensors 8 uo .. + 8 at row st, hi / lo
+        split8<0>(v, fh[0], fl[0]);
+        split8<1>(v, fh[1], fl[1]);
+        split8<2>(v, fh[2], fl[2]);
+        split8<3>(v, fh[3], fl[3]);
+        if (t0 + GSS < tend) load(t0 + GSS);
+        __syncthreads();   // the previous stage's image and O reads are done
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int o = ((4 * sq + j) * GSS + st) * BRS + 8 * uo;
+            *reinterpret_cast<uint4*>(&IH[o]) = fh[j];
+            *reinterpret_cast<uint4*>(&IL[o]) = fl[j];
+        }
+        __syncthreads();
+        f32x4 acc[4][2];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const int o = ((4 * w + cc) * GSS + i16) * BRS + 8 * kq;
+            const uint4 bh = *reinterpret_cast<const uint4*>(&IH[o]);
+            const uint4 bl = *reinterpret_cast<const uint4*>(&IL[o]);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                f32x4 c = {0.f, 0.f, 0.f, 0.f};
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][0]),
+                                                           __builtin_bit_cast(bf16x8, bh), c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][1]),
+                                                           __builtin_bit_cast(bf16x8, bh), c, 0, 0, 0);
+                acc[cc][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][0]),
+                                                                    __builtin_bit_cast(bf16x8, bl), c, 0, 0, 0);
+            }
+        }
+        // lane holds D_c[u = 16 m + 4 kq + i][t = i16] for the wave's 4 channels
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            if (m) __syncthreads();   // the first half's O reads are done
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    O[((4 * kq + i) * GSS + i16) * ORS + 4 * w + cc] = acc[cc][m][i];
+            __syncthreads();
+            // 16 tensors x 16 rows x 8 quads = 2048 pieces, 4 per thread: u = 16 m + (p >> 7)
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int p = it * GWT + tid;
+                const int ul = p >> 7, tt = (p >> 3) & 15, q = p & 7;
+                const int u = 16 * m + ul;
+                if (u < a.nu) {
+                    float4 o = *reinterpret_cast<const float4*>(&O[(ul * GSS + tt) * ORS + 4 * q]);
+                    const size_t off = (size_t)a.uid[u] * a.tstride + ((size_t)b * a.T + t0 + tt) * C + c0 + 4 * q;
+                    const float* cg = (const float*)a.cg[u];
+                    if (cg) {
+                        const float4 g = *reinterpret_cast<const float4*>(cg + ((size_t)b * a.T + t0 + tt) * C + c0 + 4 * q);
+                        o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
+                    }
+                    *reinterpret_cast<float4*>((float*)a.actw + off) = o;
+                }
+            }
+        }
+    }
+}
+
+}  // namespace
+
+void launch_gram_fwd_s(const GramArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_gram_fwd_s, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+}
+void launch_gram_bwd_s(const GramArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_gram_bwd_s, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+}
+
+}  // namespace ast

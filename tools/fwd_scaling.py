@@ -8,7 +8,7 @@ import torch
 from audio_style_transfer_amd.engine import StyleEngine
 T = 16384
 for B in [int(b) for b in (sys.argv[1:] or ['32', '64', '128', '256'])]:
-    eng = StyleEngine(B, T, [29], list(range(30)), precision='bf16')
+    eng = StyleEngine(B, T, [29], list(range(30)), precision=os.environ.get('PREC', 'split'))
     x = torch.randn(B, T, device='cuda') * 40
     for _ in range(2):
         eng.forward(x)

@@ -1,8 +1,8 @@
-"""Diagnostic: per-phase cycle shares of the bf16 block kernels (s_memtime stamps,
-libastyle_stamps.so built with -DASTYLE_STAMPS).  Shares, not absolute time, are meaningful.
+"""Diagnostic: per-phase cycle shares of the persistent block kernels (s_memtime stamps,
+libastyle_stamps.so built with -DASTYLE_STAMPS: python audio_style_transfer_amd/_build.py
+--stamps).  Shares, not absolute time, are meaningful.
 
-usage: stamps.py [clips] [fwd|bwd]   (bwd runs one loss+grad; the forward kernel's slots are 0-2,
-the backward's 4-7)"""
+usage: stamps.py [clips] [fwd|bwd] [bf16|split]   (bwd runs one loss+grad)"""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ.setdefault('ASTYLE_LIB', os.path.join(ROOT, 'audio_style_transfer_amd', 'libastyle_stamps.so'))
@@ -12,8 +12,9 @@ from audio_style_transfer_amd.engine import StyleEngine
 from audio_style_transfer_amd import _lib
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 mode = sys.argv[2] if len(sys.argv) > 2 else 'fwd'
+prec = sys.argv[3] if len(sys.argv) > 3 else 'split'
 T = 16384
-eng = StyleEngine(B, T, [29], list(range(30)), precision='bf16')
+eng = StyleEngine(B, T, [29], list(range(30)), precision=prec)
 x = torch.randn(B, T, device='cuda') * 40
 if mode == 'bwd':
     eng.set_targets(torch.randn(T, 128) * 0.1, torch.randn(*eng.style_shape) * 0.01)
@@ -26,11 +27,20 @@ lib.ast_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
 run(); torch.cuda.synchronize()
 lib.ast_debug_stamps(None)
 v = buf.cpu().tolist()
-names = ['fwd: top wait + barrier', 'fwd: GEMM1 + epi2 of prev + DMA', 'fwd: epi1 + GEMM2', '-',
-         'bwd: top wait + barrier', 'bwd: step 1 + g_u + barrier', 'bwd: step 2 + DMA',
-         'bwd: step 3 (mask, +tot, +D, stores)', '-', '-', '-', '-']
-tiles = B * T // 128 * 30 / 256   # tiles per CU over the 30 block launches
-for lo, hi in ((0, 4), (4, 8)):
+if prec == 'bf16':
+    names = ['fwd: top wait + barrier', 'fwd: GEMM1 + epi2 of prev + DMA', 'fwd: epi1 + GEMM2', '-',
+             'bwd: top wait + barrier', 'bwd: step 1 + g_u + barrier', 'bwd: step 2 + DMA',
+             'bwd: step 3 (mask, +tot, +D, stores)', '-', '-', '-', '-']
+    tiles = B * T // 128 * 30 / 256   # tiles per CU over the 30 block launches
+    groups = ((0, 4), (4, 8))
+else:
+    names = ['fwd: top wait + B1 + DMA issue', 'fwd: convert + B2', 'fwd: GEMM1',
+             'fwd: epi1 + B3 + v + B4', 'fwd: GEMM2', 'fwd: epi2 (+stores)',
+             'bwd: top wait + B1 + DMA issue', 'bwd: convert + B2', 'bwd: step 1 + g_u + B3 + B4',
+             'bwd: step 2', 'bwd: epilogue (+stores)', '-']
+    tiles = B * T // 64 * 30 / 256
+    groups = ((0, 6), (6, 11))
+for lo, hi in groups:
     tot = sum(v[lo:hi])
     for n, c in zip(names[lo:hi], v[lo:hi]):
         if c:
