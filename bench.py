@@ -5,68 +5,122 @@ Gram over all 30 layers, content layer 29, lambda 100, gamma 0).
 
 One step = one loss+grad evaluation of every clip (encoder fwd -> Gram -> losses -> backward
 to the audio, ast_loss_grad) + the fused Adam update of the audio (ast_adam_step_dev), inputs
-already resident in HBM, replayed from a captured HIP graph (--graph 1, default).  N GPUs = N processes (torch.distributed.run), each owning its own
-256 clips: weak scaling, no collective in the step; the barrier/max-over-ranks
-timing is the only cross-rank traffic.
+already resident in HBM, replayed from a captured HIP graph (--graph 1, default).
+
+Precision (the headline): 'split' = configs[2] as stated with the reference's fp32 encoder
+arithmetic kept: fp32 storage, encoder GEMMs on split-fp16 MFMA (each fp32 operand as two
+fp16 halves, 22 significant bits, fp32 accumulation), Gram on bf16 MFMA.  Its gradient is
+checked live against the committed fp64 oracle gradient (tests/golden) on every run, beside
+the fp32 and bf16 modes' (side keys).
+
+N GPUs = N processes, one per GPU, each owning its own 256 clips: weak scaling, no collective
+in the step; the barrier/max-over-ranks timing is the only cross-rank traffic.
+`python bench.py --gpus N` starts the N ranks itself (torch.distributed.run, before any GPU
+call) unless it already runs under a launcher (WORLD_SIZE set, which must equal N).
 
 Prints ONE JSON line on rank 0.  value = (clips processed by all ranks / 256) / seconds.
 """
 from __future__ import annotations
 
 import argparse
+import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32 MFMA (= vector) peak
-BF16_MFMA_PEAK_TFLOPS = 2500.0    # dense bf16
+F16_MFMA_PEAK_TFLOPS = 2500.0     # dense bf16 / fp16
 HBM_PEAK_GBS = 8000.0
+METRIC = 'style-transfer iters/sec, 256x16384-sample batch, 30-layer WaveNet encoder'
+PREC_NOTE = {
+    'split': 'fp32 storage; encoder GEMMs on split-fp16 MFMA (two fp16 halves per fp32 operand, '
+             'three products, fp32 accumulation); Gram on bf16 MFMA (two-term bf16 operands)',
+    'fp32': 'fp32 storage + fp32 MFMA (v_mfma_f32_32x32x2_f32)',
+    'bf16': 'bf16 storage + bf16 MFMA, fp32 accumulation (bf16 activations through 30 residual '
+            'blocks: ~10 % gradient error, see grad_rel_l2)',
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--clips', type=int, default=256, help='clips per GPU (batch)')
     ap.add_argument('--T', type=int, default=16384)
-    ap.add_argument('--precision', default='bf16', choices=['fp32', 'bf16'],
-                    help='bf16: bf16 storage + bf16 MFMA, fp32 accumulation (throughput mode); '
-                         'fp32: fp32 storage + fp32 MFMA (parity mode)')
-    ap.add_argument('--fp32-steps', type=int, default=2,
-                    help='also time the fp32 parity mode for this many steps (N=1 only; 0 = off)')
-    ap.add_argument('--lbfgs-steps', type=int, default=5,
-                    help='side measurement: steps of the device L-BFGS-B mode (0: skip)')
+    ap.add_argument('--precision', default='split', choices=['split', 'fp32', 'bf16'])
+    ap.add_argument('--side-steps', type=int, default=3,
+                    help='N=1 side keys: steps of the fp32 / bf16 modes, the device L-BFGS-B mode '
+                         'and the 1-clip configs[1] lines (0 = off)')
     ap.add_argument('--gatys', action='store_true',
                     help='configs[4]: Gatys [L,128,128] Gram instead of the channel-wise one')
     ap.add_argument('--lr', type=float, default=2.0)
     ap.add_argument('--graph', type=int, default=1,
                     help='1: replay the step from a captured HIP graph (default); 0: eager launches')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0,
-                    help='CPU oracle sample budget (0 disables)')
+                    help='CPU baseline sample budget (0 disables)')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'),
                     help='per-launch HBM bytes measured by rocprofv3 --pmc (see DESIGN.md)')
-    return ap.parse_args()
+    ap.add_argument('--engine', default='audio_style_transfer_amd.engine:StyleEngine',
+                    help='module:Class of the engine (tests substitute a CPU stand-in)')
+    ap.add_argument('--backend', default='nccl', help='torch.distributed backend for N > 1')
+    return ap.parse_args(argv)
 
 
-def dist_setup():
+# ----------------------------------------------------------------------------- launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(argv):
+    """--gpus N without a launcher: start N ranks under torch.distributed.run as a child
+    process (nothing here has touched the GPU) and return its exit code."""
+    args = parse(argv)
+    ws_env = os.environ.get('WORLD_SIZE')
+    if ws_env is not None:
+        if int(ws_env) != args.gpus:
+            print('bench.py: WORLD_SIZE=%s but --gpus %d' % (ws_env, args.gpus), file=sys.stderr)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(args.gpus), '--master-addr', '127.0.0.1',
+           '--master-port', str(_free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '0'))
+    return subprocess.call(cmd, env=env)
+
+
+# ----------------------------------------------------------------------------- ranks
+def dist_setup(args):
+    import torch
     ws = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.backend == 'nccl':
+        torch.cuda.set_device(local)
+        dev = torch.device('cuda', local)
+    else:
+        dev = torch.device('cpu')
     if ws > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    else:
-        torch.cuda.set_device(0)
-    return ws, rank, local
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
+    return ws, rank, dev
 
 
 def barrier(ws):
@@ -75,10 +129,22 @@ def barrier(ws):
         dist.barrier()
 
 
+def sync(dev):
+    import torch
+    if dev.type == 'cuda':
+        torch.cuda.synchronize(dev)
+
+
+def engine_class(spec):
+    mod, cls = spec.split(':')
+    return getattr(importlib.import_module(mod), cls)
+
+
 def make_problem(eng, clips, T, dev):
     """Synthetic per-clip targets for the global clip indices `clips`: content
     clip c_g, style clip s_g; phi_c = emb_c(c_g); phi_s = l2norm(G^(c_g) + G^(s_g) - G^(c_g))
     (methods.py:207-212 with one clip per file); x0 = c_g + 4 N(0,1) (seeded per clip)."""
+    import torch
     from audio_style_transfer_amd.shard import shard_inputs
     cont, sty, x0 = shard_inputs(clips, T)
     cont = torch.tensor(cont, device=dev)
@@ -91,93 +157,239 @@ def make_problem(eng, clips, T, dev):
     return torch.tensor(x0, device=dev)
 
 
-def cpu_baseline(T, budget_s):
-    """Time the CPU oracle (oracle/astyle_oracle.py, numpy fp32, host BLAS threads) on a
-    bounded sample of the same workload: whole loss+grad evaluations of single clips."""
-    from oracle import astyle_oracle as O
-    from audio_style_transfer_amd.weights import synthetic_weights, synthetic_clips
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get('num_threads', 1) for i in threadpool_info()] or [1])
-    except Exception:
-        cores = 1
-    W = synthetic_weights(0)
-    kw = dict(cont_ids=[29], style_ids=list(range(30)), gatys=False, nb_channels=128,
-              cnt_channels=128)
-    xc = O.mu_law_numpy(synthetic_clips(1, T, 1000)[0])
-    ext, _ = O.encoder_forward(xc, W, 30, dtype=np.float32)
-    phi_c = O.content_embeds(ext, [29], 128)
-    phi_s = O.style_embeds(ext, list(range(30)))
-    x = xc + np.random.default_rng(0).normal(0, 4, T)
-    n = 0
-    t0 = time.time()
-    while True:
-        O.loss_and_grad(x, W, phi_c=phi_c, phi_s=phi_s, lambd=100.0, dtype=np.float32, **kw)
-        n += 1
-        el = time.time() - t0
-        if el >= budget_s or n >= 64:
-            break
-    clip_evals_per_s = n / el
-    return {'value': clip_evals_per_s / 256.0, 'unit': 'iters/s (256x%d batch)' % T,
-            'cores': int(cores), 'kind': 'port',
-            'sample': '%d full loss+grad evaluations of one %d-sample clip (numpy fp32 oracle, '
-                      '30 blocks, ours-Gram L=30) in %.1f s = %.3f clip-evals/s; scaled to the '
-                      '256-clip batch' % (n, T, el, clip_evals_per_s),
-            'clip_evals_per_s': clip_evals_per_s}
-
-
-def run(args, precision, steps, warmup, ws, rank, dev, graph):
+def run(args, Eng, precision, steps, warmup, ws, rank, dev, graph, clips=None, gatys=None):
     """Build the engine, warm up, time `steps` steps (barrier + sync on both sides, max over
     ranks).  A step is one AdamLoop step (ast_loss_grad + device-counter Adam), replayed from
     a captured HIP graph when `graph`.  The per-kernel-family breakdown comes from HIP events
     of 2 extra eager steps (events are not recorded inside a graph).  Returns (seconds,
-    engine timing dict, first loss, last loss)."""
-    from audio_style_transfer_amd.engine import StyleEngine, AdamLoop
+    engine timing dict, first loss, last loss, non-finite clips)."""
+    import torch
+    from audio_style_transfer_amd.engine import AdamLoop
     from audio_style_transfer_amd.shard import clip_range, max_over_ranks
-    B, T = args.clips, args.T
-    eng = StyleEngine(B, T, [29], list(range(30)), precision=precision, device=dev,
-                      lambd=100.0, gatys=args.gatys)
+    B = clips or args.clips
+    T = args.T
+    eng = Eng(B, T, [29], list(range(30)), precision=precision, device=dev, lambd=100.0,
+              gatys=args.gatys if gatys is None else gatys)
     x = make_problem(eng, clip_range(ws * B, ws, rank), T, dev)
-    loop = AdamLoop(eng, x, lr=args.lr, graph=graph)
+    loop = AdamLoop(eng, x, lr=args.lr, graph=graph and dev.type == 'cuda')
     for _ in range(warmup):
         loop.step()
-    torch.cuda.synchronize()
+    sync(dev)
     first_loss = loop.parts[:, 0].mean().item()
     barrier(ws)
-    torch.cuda.synchronize()
+    sync(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         loop.step()
-    torch.cuda.synchronize()
+    sync(dev)
     barrier(ws)
     el = time.perf_counter() - t0
     el = max_over_ranks(el, ws, device=dev)
     last_loss = loop.parts[:, 0].mean().item()
-    if not np.isfinite(last_loss):
-        raise SystemExit('non-finite loss')
+    bad = int((~torch.isfinite(loop.parts[:, 0])).sum().item())   # per-clip non-finite flag
     eng.timing(True)
     for _ in range(2):
         loop._eager()
-    torch.cuda.synchronize()
+    sync(dev)
     tm = eng.timing_read()
     eng.timing(False)
     del loop, x
     eng.close()
-    torch.cuda.empty_cache()
-    return el, tm, first_loss, last_loss
+    if dev.type == 'cuda':
+        torch.cuda.empty_cache()
+    return el, tm, first_loss, last_loss, bad
 
 
-def run_lbfgs(args, steps, dev):
-    """Side measurement (rank 0, N=1): the reference's optimiser, scipy's L-BFGS-B restated on
-    the device (ast_lbfgs_*), over the same 256-clip workload.  A step is one evaluation of every
+def grad_check(Eng, precision, dev):
+    """d loss / d x of one 2048-sample clip against the committed fp64 oracle gradient
+    (tests/golden: 'ours' = 30 style layers, content layer 25, the oracle's own targets)."""
+    import torch
+    g = np.load(os.path.join(ROOT, 'tests', 'golden', 'oracle_T2048.npz'))
+    tg = np.load(os.path.join(ROOT, 'tests', 'golden', 'oracle_T2048_targets.npz'))
+    eng = Eng(1, 2048, [25], list(range(30)), precision=precision, device=dev, lambd=100.0)
+    eng.set_targets(torch.tensor(tg['ours_phi_c']), torch.tensor(tg['ours_phi_s']))
+    parts, grad = eng.loss_grad(torch.tensor(g['ours_x'][None], dtype=torch.float32, device=dev))
+    grad = grad.cpu().double().numpy()[0]
+    loss = float(parts[0, 0])
+    eng.close()
+    ref = g['ours_grad']
+    return {'grad_rel_l2': float(np.linalg.norm(grad - ref) / np.linalg.norm(ref)),
+            'loss_rel': abs(loss - float(g['ours_parts'][0])) / abs(float(g['ours_parts'][0]))}
+
+
+def cpu_baseline(T, budget_s):
+    """Time the torch-CPU fp32 restatement of the reference path (oracle/torch_restatement.py:
+    F.conv1d forward, autograd backward; the reference's TF-CPU path needs TensorFlow, absent
+    here) on this host's cores, on a bounded sample of the same workload: whole loss+grad
+    evaluations of single clips, scaled to the 256-clip batch."""
+    import torch
+    from oracle import torch_restatement as TR
+    from audio_style_transfer_amd.weights import synthetic_weights, synthetic_clips
+    from audio_style_transfer_amd.utils import mu_law_numpy
+    cores = int(os.environ.get('OMP_NUM_THREADS', '0')) or os.cpu_count()
+    cores = min(cores, os.cpu_count())
+    torch.set_num_threads(cores)
+    W = synthetic_weights(0)
+    kw = dict(cont_ids=[29], style_ids=list(range(30)))
+    xc = mu_law_numpy(synthetic_clips(1, T, 1000)[0]).astype(np.float64)
+    phi_c = np.zeros((T, 128), np.float32)
+    phi_s = np.zeros((128, 30, 30), np.float32)
+    x = xc + np.random.default_rng(0).normal(0, 4, T)
+    TR.cpu_step(x, W, phi_c=phi_c, phi_s=phi_s, **kw)      # warm-up (allocator, threads)
+    n = 0
+    t0 = time.time()
+    while True:
+        TR.cpu_step(x, W, phi_c=phi_c, phi_s=phi_s, **kw)
+        n += 1
+        el = time.time() - t0
+        if el >= budget_s or n >= 200:
+            break
+    clip_evals_per_s = n / el
+    return {'value': clip_evals_per_s / 256.0, 'unit': 'iters/s (256x%d batch)' % T,
+            'cores': int(cores), 'host_cpus': os.cpu_count(), 'kind': 'port',
+            'sample': '%d loss+grad evaluations of one %d-sample clip in %.1f s = %.3f clip-evals/s '
+                      '(torch-CPU fp32 restatement: conv1d forward + autograd backward, 30 blocks, '
+                      'ours-Gram L=30, STFT regulariser evaluated as TF does); scaled to the '
+                      '256-clip batch' % (n, T, el, clip_evals_per_s),
+            'clip_evals_per_s': clip_evals_per_s,
+            'note': 'a reported baseline, not the target'}
+
+
+def block_roofline(precision, B, T, fwd_ms, bwd_ms, traffic):
+    """Roofline of the block kernels, one fwd and one bwd launch (all clips).  Algorithmic
+    bytes: fwd reads e_l and writes e_{l+1} (2A), bwd reads the chain and D_l and
+    writes the chain (3A), A = B T 128 x element size; plus the relu-mask words (16 B per row
+    written by the fwd, 32 B read by the bwd).  FLOP: 131072 per row (2 (384 + 128) 128); the
+    split mode executes three MFMA products per FLOP."""
+    esz = 2.0 if precision == 'bf16' else 4.0
+    rows = float(B) * T
+    A = rows * 128 * esz
+    fbytes = 2 * A + 32 * rows
+    bbytes = 3 * A + 32 * rows
+    flops = 131072.0 * rows
+    mult = 3.0 if precision == 'split' else 1.0
+    peak = FP32_MFMA_PEAK_TFLOPS if precision == 'fp32' else F16_MFMA_PEAK_TFLOPS
+
+    def one(ms, nbytes, tb):
+        mf = flops * mult / (ms * 1e-3) / 1e12
+        gb = nbytes / (ms * 1e-3) / 1e9
+        d = {'launch_ms': ms, 'algorithmic_bytes': nbytes, 'algorithmic_flops': flops,
+             'executed_mfma_flops': flops * mult, 'mfma_TFLOPs': mf, 'mfma_frac': mf / peak,
+             'hbm_GBs': gb, 'hbm_frac': gb / HBM_PEAK_GBS, 'traffic': tb}
+        d['bound'] = 'mfma' if d['mfma_frac'] >= d['hbm_frac'] else 'hbm'
+        return d
+
+    tf = traffic or {}
+    f = one(fwd_ms, fbytes, tf.get('fwd'))
+    b = one(bwd_ms, bbytes, tf.get('bwd'))
+    bound = 'mfma' if (f['mfma_frac'] + b['mfma_frac']) >= (f['hbm_frac'] + b['hbm_frac']) else 'hbm'
+    if bound == 'mfma':
+        roof = {'bound': 'mfma', 'achieved': (f['mfma_TFLOPs'] + b['mfma_TFLOPs']) / 2, 'peak': peak,
+                'unit': 'TFLOP/s'}
+    else:
+        roof = {'bound': 'hbm', 'achieved': (f['hbm_GBs'] + b['hbm_GBs']) / 2, 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s'}
+    roof['frac'] = roof['achieved'] / roof['peak']
+    roof['traffic'] = ((tf['fwd'] + tf['bwd']) / 2) if tf.get('fwd') and tf.get('bwd') else None
+    roof.update({'kernel': 'k_block_fwd*/k_block_bwd* (fused dilated conv + 1x1 + epilogues), '
+                           'mean of one fwd and one bwd launch; fwd / bwd below',
+                 'fwd': f, 'bwd': b})
+    return roof
+
+
+def rank_main(args):
+    import torch
+    ws, rank, dev = dist_setup(args)
+    Eng = engine_class(args.engine)
+    B, T, L = args.clips, args.T, 30
+    el, tm, first_loss, last_loss, bad = run(args, Eng, args.precision, args.steps, args.warmup,
+                                             ws, rank, dev, bool(args.graph))
+    side = {}
+    if ws == 1 and args.side_steps > 0 and dev.type == 'cuda':
+        for p in ('fp32', 'bf16', 'split'):
+            if p == args.precision:
+                continue
+            e2, tm2, _, _, _ = run(args, Eng, p, args.side_steps, 1, ws, rank, dev, bool(args.graph))
+            calls = max(tm2['calls'], 1)
+            side[p + '_mode'] = {'value': B * args.side_steps / 256.0 / e2, 'unit': 'iters/s',
+                                 'steps': args.side_steps, 'precision': PREC_NOTE[p],
+                                 'kernels_ms_per_step': {k[:-3]: tm2[k] / calls for k in
+                                                         ('block_fwd_ms', 'block_bwd_ms',
+                                                          'gram_fwd_ms', 'gram_bwd_ms', 'other_ms')},
+                                 **grad_check(Eng, p, dev)}
+        for p in ('split', 'fp32'):     # configs[1]: one 16384-sample clip
+            e1, _, _, _, _ = run(args, Eng, p, 10 * args.side_steps, 2, ws, rank, dev,
+                                 bool(args.graph), clips=1, gatys=False)
+            side['config1_%s' % p] = {'value': 10 * args.side_steps / e1, 'unit': 'iters/s',
+                                      'note': 'configs[1]: 1 clip x %d, channel-wise Gram, 30 '
+                                              'blocks, %s' % (T, PREC_NOTE[p])}
+        side['lbfgs_mode'] = run_lbfgs(args, Eng, 2 * args.side_steps, dev)
+    if rank != 0:
+        barrier(ws)
+        return None
+    value = ws * B * args.steps / 256.0 / el
+    calls = max(tm['calls'], 1)
+    nblk = max(tm['blocks'], 1)
+    fwd_ms = tm['block_fwd_ms'] / (calls * nblk)
+    bwd_ms = tm['block_bwd_ms'] / (calls * nblk)
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get('precision') == args.precision and tj.get('clips') == B and tj.get('T') == T:
+            traffic = {'fwd': tj['fwd_bytes_per_launch'], 'bwd': tj['bwd_bytes_per_launch']}
+    except Exception:
+        traffic = None
+    gram_fwd_ms = tm['gram_fwd_ms'] / calls
+    gram_bwd_ms = tm['gram_bwd_ms'] / calls
+    gbytes = L * B * T * 128 * (2.0 if args.precision == 'bf16' else 4.0)
+    out = {
+        'metric': METRIC, 'value': value, 'unit': 'iters/s', 'n_gpus': ws, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': el / args.steps * 1e3,
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': {'split': 'fp32 (split-f16 MFMA)', 'fp32': 'fp32', 'bf16': 'bf16'}[args.precision],
+        'data': 'synthetic (seeded sinusoid+noise clips, seeded uniform_unit_scaling weights)',
+        'config': {'workload': ('configs[4]: %dx%d clips per GPU, 30-block encoder, Gatys Gram '
+                                if args.gatys else
+                                'configs[2]: %dx%d clips per GPU, 30-block encoder, ours-Gram ')
+                               % (B, T) + 'L=30, cont_lyrs [29], lambd 100, gamma 0, Adam step',
+                   'global_batch_clips': ws * B, 'T': T, 'parallelism': 'clip-sharded x%d' % ws,
+                   'precision': args.precision, 'precision_detail': PREC_NOTE[args.precision],
+                   'hip_graph': bool(args.graph)},
+        'clip_iters_per_s': value * 256.0,
+        'roofline': block_roofline(args.precision, B, T, fwd_ms, bwd_ms, traffic),
+        'kernels_ms_per_step': {'block_fwd': tm['block_fwd_ms'] / calls,
+                                'block_bwd': tm['block_bwd_ms'] / calls,
+                                'gram_fwd': gram_fwd_ms, 'gram_bwd': gram_bwd_ms,
+                                'other': tm['other_ms'] / calls},
+        'gram_roofline': {'bound': 'hbm', 'fwd_achieved_GBs': gbytes / (gram_fwd_ms * 1e-3) / 1e9,
+                          'bwd_achieved_GBs': 2 * gbytes / (gram_bwd_ms * 1e-3) / 1e9,
+                          'peak': HBM_PEAK_GBS},
+        'loss_first_last': [first_loss, last_loss],
+        'nonfinite_clips': bad,
+    }
+    if dev.type == 'cuda':
+        out.update(grad_check(Eng, args.precision, dev))
+    out.update(side)
+    if ws == 1 and args.cpu_baseline_seconds > 0:
+        out['cpu_baseline'] = cpu_baseline(T, args.cpu_baseline_seconds)
+    print(json.dumps(out), flush=True)
+    barrier(ws)
+    return out
+
+
+def run_lbfgs(args, Eng, steps, dev):
+    """Side measurement (N=1): the reference's optimiser, scipy's L-BFGS-B restated on the
+    device (ast_lbfgs_*), over the same 256-clip workload.  A step is one evaluation of every
     clip (ast_loss_grad) + one ast_lbfgs_step, replayed from a HIP graph; the L-BFGS-B kernel's
     own time comes from HIP events around eager launches on the engine's stream."""
     import ctypes
-    from audio_style_transfer_amd.engine import StyleEngine, LbfgsLoop
+    import torch
+    from audio_style_transfer_amd.engine import LbfgsLoop
     from audio_style_transfer_amd.shard import clip_range
     B, T = args.clips, args.T
-    eng = StyleEngine(B, T, [29], list(range(30)), precision=args.precision, device=dev,
-                      lambd=100.0, gatys=args.gatys)
+    eng = Eng(B, T, [29], list(range(30)), precision=args.precision, device=dev, lambd=100.0,
+              gatys=args.gatys)
     x = make_problem(eng, clip_range(B, 1, 0), T, dev)
     loop = LbfgsLoop(eng, maxiter=100, graph=bool(args.graph))
     loop.begin(x.double())
@@ -209,104 +421,18 @@ def run_lbfgs(args, steps, dev):
     return {'value': B * steps / 256.0 / el, 'unit': 'iters/s', 'steps': steps,
             'lbfgs_step_ms': ms, 'clips_running': int((info[:, 0] != 0).sum()),
             'note': 'device L-BFGS-B (scipy semantics: m 10, dcsrch line search, maxiter 100) '
-                    'instead of Adam, same workload; one iter = one loss+grad evaluation of every '
-                    'clip + the L-BFGS-B update'}
+                    'instead of Adam, same workload and precision; one iter = one loss+grad '
+                    'evaluation of every clip + the L-BFGS-B update'}
 
 
-def main():
-    args = parse()
-    ws, rank, local = dist_setup()
-    dev = torch.device('cuda', local)
-    B, T = args.clips, args.T
-    L = 30
-    el, tm, first_loss, last_loss = run(args, args.precision, args.steps, args.warmup, ws,
-                                        rank, dev, args.graph)
-    fp32_side = None
-    if args.fp32_steps > 0 and args.precision != 'fp32' and ws == 1:
-        el32, _, _, _ = run(args, 'fp32', args.fp32_steps, 1, ws, rank, dev, args.graph)
-        fp32_side = {'value': B * args.fp32_steps / 256.0 / el32, 'unit': 'iters/s',
-                     'steps': args.fp32_steps,
-                     'note': 'same workload with fp32 storage + fp32 MFMA (parity mode: grad '
-                             'within 2e-3 rel-L2 of the fp64 oracle)'}
-    lbfgs_side = None
-    if args.lbfgs_steps > 0 and ws == 1:
-        lbfgs_side = run_lbfgs(args, args.lbfgs_steps, dev)
-    if rank != 0:
-        barrier(ws)
-        return
-    value = ws * B * args.steps / 256.0 / el
-    calls = max(tm['calls'], 1)
-    nblk = tm['blocks']
-    fwd_ms = tm['block_fwd_ms'] / (calls * nblk)
-    bwd_ms = tm['block_bwd_ms'] / (calls * nblk)
-    launch_ms = (fwd_ms + bwd_ms) / 2
-    esz = 4.0 if args.precision == 'fp32' else 2.0
-    A = B * T * 128 * esz                          # one activation tensor, all clips
-    flops_per_launch = 131072.0 * T * B            # 2*(384+128)*128 flop per row, fwd or bwd
-    bytes_per_launch = 2.5 * A                     # fwd 2A (read e_l, write e_l+1), bwd 3A
-    traffic = None
-    try:
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        if (tj.get('precision') == args.precision and tj.get('clips') == B and tj.get('T') == T):
-            traffic = tj['block_bytes_per_launch']
-    except Exception:
-        traffic = None
-    if args.precision == 'fp32':
-        # fp32: 96 flop/B on the dilated conv, above the fp32 ridge -> MFMA-bound
-        achieved = flops_per_launch / (launch_ms * 1e-3) / 1e12
-        roof = {'bound': 'mfma', 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS,
-                'unit': 'TFLOP/s', 'frac': achieved / FP32_MFMA_PEAK_TFLOPS}
-    else:
-        # bf16 storage: 192 flop/B fwd (below the 312 flop/B bf16 ridge) -> HBM-bound
-        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-        roof = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                'frac': achieved / HBM_PEAK_GBS}
-    roof.update({'traffic': traffic,
-                 'kernel': 'k_block_fwd*/k_block_bwd* (fused dilated conv + 1x1 + epilogues), '
-                           'mean of one fwd and one bwd launch',
-                 'algorithmic_bytes_per_launch': bytes_per_launch,
-                 'flops_per_launch': flops_per_launch,
-                 'mfma_frac': flops_per_launch / (launch_ms * 1e-3) / 1e12 /
-                              (FP32_MFMA_PEAK_TFLOPS if args.precision == 'fp32'
-                               else BF16_MFMA_PEAK_TFLOPS),
-                 'avg_launch_ms': launch_ms, 'fwd_launch_ms': fwd_ms, 'bwd_launch_ms': bwd_ms})
-    gram_fwd_ms = tm['gram_fwd_ms'] / calls
-    gram_bwd_ms = tm['gram_bwd_ms'] / calls
-    gram_bytes = L * A
-    out = {
-        'metric': 'style-transfer iters/sec, 256x16384-sample batch, 30-layer WaveNet encoder',
-        'value': value, 'unit': 'iters/s', 'n_gpus': ws, 'steps': args.steps,
-        'warmup': args.warmup, 'ms_per_step': el / args.steps * 1e3,
-        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-        'dtype': args.precision,
-        'data': 'synthetic (seeded sinusoid+noise clips, seeded uniform_unit_scaling weights)',
-        'config': {'workload': ('configs[4]: %dx%d clips per GPU, 30-block encoder, Gatys Gram '
-                                if args.gatys else
-                                'configs[2]: %dx%d clips per GPU, 30-block encoder, ours-Gram ')
-                               % (B, T) + 'L=30, cont_lyrs [29], lambd 100, gamma 0, Adam step',
-                   'global_batch_clips': ws * B, 'T': T, 'parallelism': 'clip-sharded x%d' % ws,
-                   'precision': args.precision, 'hip_graph': bool(args.graph)},
-        'clip_iters_per_s': value * 256.0,
-        'roofline': roof,
-        'kernels_ms_per_step': {'block_fwd': tm['block_fwd_ms'] / calls,
-                                'block_bwd': tm['block_bwd_ms'] / calls,
-                                'gram_fwd': gram_fwd_ms, 'gram_bwd': gram_bwd_ms,
-                                'other': tm['other_ms'] / calls},
-        'gram_roofline': {'bound': 'hbm', 'fwd_achieved_GBs': gram_bytes / (gram_fwd_ms * 1e-3) / 1e9,
-                          'bwd_achieved_GBs': 2 * gram_bytes / (gram_bwd_ms * 1e-3) / 1e9,
-                          'peak': HBM_PEAK_GBS},
-        'loss_first_last': [first_loss, last_loss],
-    }
-    if fp32_side:
-        out['fp32_mode'] = fp32_side
-    if lbfgs_side:
-        out['lbfgs_mode'] = lbfgs_side
-    if ws == 1 and args.cpu_baseline_seconds > 0:
-        out['cpu_baseline'] = cpu_baseline(T, args.cpu_baseline_seconds)
-    print(json.dumps(out), flush=True)
-    barrier(ws)
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    rc = launch(argv)
+    if rc is not None:
+        return rc
+    rank_main(parse(argv))
+    return 0
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

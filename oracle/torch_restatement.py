@@ -1,4 +1,6 @@
-"""Independent torch-autograd restatement of the reference loss (test infrastructure only).
+"""CPU ORACLE — TEST INFRASTRUCTURE ONLY.  Independent torch-autograd restatement of the
+reference loss: imported by tests/ (it pins astyle_oracle.py's hand-derived gradient) and timed
+by bench.py's cpu_baseline leg (the reference's TF-CPU path is not runnable here: no TF).
 
 Written separately from ``oracle/astyle_oracle.py`` (channels-first ``F.conv1d`` with
 symmetric ``padding=dilation``, autograd instead of hand-written backward, ``torch.stft``)
@@ -68,6 +70,16 @@ def loss_fn(x, W, *, cont_ids, style_ids, phi_c, phi_s, lambd=100.0, gamma=0.0, 
     reg = torch.mean(_abs_tf(S.real) + _abs_tf(S.imag))
     total = content + lambd * style + gamma * reg
     return total, content, style, reg
+
+
+def cpu_step(x, W, *, cont_ids, style_ids, phi_c, phi_s, lambd=100.0, dtype=torch.float32):
+    """One loss+grad evaluation of one clip (the reference's CPU path restated: fp32 conv1d
+    forward, autograd backward to x).  Returns (total, grad [T])."""
+    xt = torch.as_tensor(x, dtype=dtype).detach().clone().requires_grad_(True)
+    total, _, _, _ = loss_fn(xt, W, cont_ids=cont_ids, style_ids=style_ids, phi_c=phi_c,
+                             phi_s=phi_s, lambd=lambd, dtype=dtype)
+    g, = torch.autograd.grad(total, xt)
+    return float(total), g
 
 
 def stft_reg(x):

@@ -10,7 +10,8 @@ The reference's text is NOT committed; only the input/output vectors are
 (``reference_vectors.npz`` / ``reference_paths.json``).
 
 Part 2 — oracle vectors at small T (``oracle_T2048.npz``): inputs, loss parts and the
-fp64 gradient of ``oracle/astyle_oracle.py``, for the GPU parity tests.  The oracle itself is
+fp64 gradient of ``oracle/astyle_oracle.py``, for the GPU parity tests; the 'ours' targets
+(``oracle_T2048_targets.npz``, float32) for bench.py's per-precision gradient check.  The oracle itself is
 "parity unpinned" against TF (see its header).
 
 Usage:  python tests/golden/make_golden.py
@@ -136,6 +137,9 @@ def oracle_vectors():
         rng = np.random.default_rng(7)
         x = (O.mu_law_numpy(synthetic_clips(1, T, 42)[0]) + rng.normal(0, 4, T))
         parts, g = O.loss_and_grad(x, W, phi_c=phi_c, phi_s=phi_s, lambd=100.0, gamma=0.0, **kw)
+        if tag == 'ours':   # targets for bench.py's per-precision gradient check
+            np.savez_compressed(os.path.join(HERE, 'oracle_T2048_targets.npz'),
+                                ours_phi_c=phi_c.astype(np.float32), ours_phi_s=phi_s.astype(np.float32))
         out[tag + '_x'] = x
         out[tag + '_parts'] = parts
         out[tag + '_grad'] = g

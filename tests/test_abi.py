@@ -75,7 +75,8 @@ def _ws(**kw):
 def test_workspace_scales_with_precision_and_blocks():
     rc32, n32, _ = _ws(precision=0)
     rc16, n16, _ = _ws(precision=1)
-    assert rc32 == 0 and rc16 == 0 and n16 < n32
+    rcs, ns, _ = _ws(precision=2)
+    assert rc32 == 0 and rc16 == 0 and rcs == 0 and n16 < n32 < ns   # split: + fp16 fragments
     # stack 0 + content 25 runs 26 blocks (TF prunes the rest)
     rc, n26, _ = _ws(cont=[25], style=list(range(10)))
     assert rc == 0 and n26 < n32
@@ -85,7 +86,7 @@ def test_workspace_scales_with_precision_and_blocks():
     (dict(T=1000), 'multiple of 512'),
     (dict(cont=[32]), 'content layer ids'),
     (dict(style=[31]), 'style layer ids'),
-    (dict(precision=2), 'precision'),
+    (dict(precision=3), 'precision'),
     (dict(cnt=0), 'cnt_channels'),
 ])
 def test_invalid_configs_fail_loudly(kw, msg):

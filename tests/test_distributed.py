@@ -81,3 +81,49 @@ def test_two_rank_gloo_matches_single_process(tmp_path):
     assert gathered.shape == ref.shape
     assert np.array_equal(gathered, ref)
     assert float(np.load(tmp_path / 'max.npy')[0]) == 2.0
+
+
+# ----------------------------------------------------------------------------- bench.py
+def _bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(root, 'tests'), root]))
+    env.pop('WORLD_SIZE', None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), *args], env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{')]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+STUB = ['--engine', 'bench_stub:StubEngine', '--backend', 'gloo', '--T', '512', '--steps', '2',
+        '--warmup', '1', '--cpu-baseline-seconds', '0', '--side-steps', '0', '--graph', '0']
+
+
+def test_bench_launcher_starts_ranks():
+    """`bench.py --gpus 2` with no launcher around it starts 2 ranks itself (torch.distributed.run)
+    and rank 0 reports the whole job: n_gpus 2, 2 x clips clips, the bench's own rank logic
+    (clip shards by global index, warm-up, barrier-bracketed timing, max over ranks)."""
+    rc, out, err = _bench(['--gpus', '2', '--clips', '3', *STUB])
+    assert rc == 0, err[-2000:]
+    assert out['n_gpus'] == 2 and out['config']['global_batch_clips'] == 6, out
+    assert out['scaling'] == 'weak' and out['config']['parallelism'] == 'clip-sharded x2'
+    assert out['value'] > 0 and out['nonfinite_clips'] == 0
+
+
+def test_bench_refuses_mismatched_world_size():
+    rc, out, err = _bench(['--gpus', '4', '--clips', '2', *STUB], env_extra={'WORLD_SIZE': '2'})
+    assert rc == 2 and out is None, (rc, err)
+
+
+def test_bench_rank_results_match_single_process():
+    """Rank 0 of a 2-rank run owns global clips 0, 1 — the same clips a 1-rank run with 2 clips
+    owns — so its losses (first and last timed step) are identical: shards are built from the
+    global clip index and the step does not depend on the other rank."""
+    rc1, out1, e1 = _bench(['--gpus', '1', '--clips', '2', *STUB])
+    rc2, out2, e2 = _bench(['--gpus', '2', '--clips', '2', *STUB])
+    assert rc1 == 0 and rc2 == 0, (e1[-1000:], e2[-1000:])
+    assert out1['config']['global_batch_clips'] == 2 and out2['config']['global_batch_clips'] == 4
+    assert out1['loss_first_last'] == out2['loss_first_last']

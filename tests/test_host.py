@@ -92,7 +92,7 @@ def test_stft_regularizer_matches_oracle():
     rng = np.random.default_rng(4)
     x = rng.normal(0, 30, (2, 4096))
     x[0, :7] = 0.0                      # inv_mu_law's x == 0 branch
-    import torch_restatement as TR
+    from oracle import torch_restatement as TR
     val, g = TR.stft_reg(torch.tensor(x))
     for b in range(2):
         rv, rg = O.stft_reg(x[b])

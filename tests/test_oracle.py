@@ -11,7 +11,7 @@ from oracle import astyle_oracle as O
 from audio_style_transfer_amd import utils as U
 from audio_style_transfer_amd.weights import synthetic_clips
 
-import torch_restatement as TR
+from oracle import torch_restatement as TR
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
