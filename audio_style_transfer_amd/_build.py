@@ -20,7 +20,7 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall',
 # MFMA accumulators in arch VGPRs, where the epilogues read them without copies; their fully
 # unrolled tile loops exceed the default pragma-unroll size limit (a partly unrolled loop would
 # index the register-resident weight arrays dynamically and demote them to scratch)
-_CW = ['-mllvm', '-amdgpu-mfma-vgpr-form=1', '-mllvm', '-pragma-unroll-threshold=1000000']
+_CW = ['-mllvm', '-amdgpu-mfma-vgpr-form=1', '-mllvm', '-pragma-unroll-threshold=1000000', '-fno-slp-vectorize']
 EXTRA = {'block_fwd_bf16.hip': _CW, 'block_bwd_bf16.hip': _CW, 'block_fwd_split.hip': _CW,
          'block_bwd_split.hip': _CW}
 
@@ -34,12 +34,15 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
-    lib = LIB if not stamps else os.path.join(PKG, 'libastyle_stamps.so')
+def build(force: bool = False, verbose: bool = False, stamps: bool = False, exp: int = 0) -> str:
+    """exp > 0 (stamps builds): -DSW_EXP=exp, a timing experiment of the split block kernels
+    (drops parts of their work; results are wrong) -> libastyle_stamps_exp<exp>.so"""
+    tag = '' if not exp else '_exp%d' % exp
+    lib = LIB if not stamps else os.path.join(PKG, 'libastyle_stamps%s.so' % tag)
     if not force and not stamps and not _stale():
         return LIB
-    objdir = os.path.join(PKG, 'build' if not stamps else 'build_stamps')
-    flags = FLAGS + (['-DASTYLE_STAMPS'] if stamps else [])
+    objdir = os.path.join(PKG, 'build' if not stamps else 'build_stamps' + tag)
+    flags = FLAGS + (['-DASTYLE_STAMPS'] if stamps else []) + (['-DSW_EXP=%d' % exp] if exp else [])
     os.makedirs(objdir, exist_ok=True)
 
     def cc(src):
@@ -66,4 +69,6 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> s
 
 
 if __name__ == '__main__':
-    print(build(force='--force' in sys.argv, verbose=True, stamps='--stamps' in sys.argv))
+    exp = int(sys.argv[sys.argv.index('--exp') + 1]) if '--exp' in sys.argv else 0
+    print(build(force='--force' in sys.argv, verbose=True, stamps='--stamps' in sys.argv or exp > 0,
+                exp=exp))

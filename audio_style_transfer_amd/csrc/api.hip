@@ -105,6 +105,7 @@ struct ast_ctx {
     u16* wtsb = nullptr;                    // bf16 weight copies (precision 1)
     uint4* wtss = nullptr;                  // split-fp16 weight fragments (precision 2)
     int kd[NBLK_MAX] = {}, kr[NBLK_MAX] = {};   // their exponents
+    float wdn[NBLK_MAX] = {}, wrn[NBLK_MAX] = {}, bdm[NBLK_MAX] = {};   // operand bounds (splitwave.h)
     bool bf = false;                        // precision 1: bf16 activations/gradients
     bool split = false;                     // precision 2: fp32 storage, split-fp16 block GEMMs
     unsigned* gmax_e = nullptr;             // [nblk + 1][B] max |e_l| per clip (precision 2)
@@ -268,6 +269,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
             a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
             a.dn_log2 = (l + 1) % 10; a.nn = c.T >> a.dn_log2;
             a.kd = x->kd[l]; a.kr = x->kr[l];
+            a.wdn = x->wdn[l]; a.bdm = x->bdm[l];
             launch_block_fwd_s(a, s);
         } else if (x->bf) {
             FwdArgsC a;
@@ -368,8 +370,8 @@ const char* ast_last_error(void) { return g_err.c_str(); }
 
 // Diagnostic hook (not in astyle.h): device buffer of 12 u64 phase-cycle sums that
 // -DASTYLE_STAMPS builds of the bf16 block kernels accumulate into; NULL disables.
-int ast_debug_stamps(void* dev_u64x12) {
-    g_stamps = (unsigned long long*)dev_u64x12;
+int ast_debug_stamps(void* dev_u64x16) {
+    g_stamps = (unsigned long long*)dev_u64x16;
     return 0;
 }
 
@@ -501,6 +503,13 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                 // backward: W_d[tap][32 w + m][16 kb + 8 h + e]
                 const int k = weight_exp(host, 3 * C * C);
                 x->kd[l - 1] = k;
+                float nrm = 0.f;
+                for (int co = 0; co < C; ++co) {
+                    float sacc = 0.f;
+                    for (int i = 0; i < 3 * C; ++i) sacc += std::fabs(host[(size_t)i * C + co]);
+                    nrm = std::max(nrm, sacc);
+                }
+                x->wdn[l - 1] = nrm;
                 std::vector<uint16_t> f(3 * C * C * 2), g(3 * C * C * 2);
                 for (int w = 0; w < 4; ++w)
                     for (int tp = 0; tp < 3; ++tp)
@@ -519,7 +528,13 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
             }
             return 0;
         }
-        if (!strcmp(tail, "biases")) { if ((rc = need(C))) return rc; return put(base + BD, host, C); }
+        if (!strcmp(tail, "biases")) {
+            if ((rc = need(C))) return rc;
+            float m = 0.f;
+            for (int i = 0; i < C; ++i) m = std::max(m, std::fabs(host[i]));
+            x->bdm[l - 1] = m;
+            return put(base + BD, host, C);
+        }
     }
     if (sscanf(name, "ae_res_%d/%31s", &l, tail) == 2 && l >= 1 && l <= NBLK_MAX) {
         const size_t base = BLK_OFF + (size_t)(l - 1) * BLK_SZ;
@@ -550,6 +565,13 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                 // backward: W_r[32 w + m][16 kb + 8 h + e]
                 const int k = weight_exp(host, C * C);
                 x->kr[l - 1] = k;
+                float nrm = 0.f;
+                for (int ci = 0; ci < C; ++ci) {
+                    float sacc = 0.f;
+                    for (int co = 0; co < C; ++co) sacc += std::fabs(host[(size_t)ci * C + co]);
+                    nrm = std::max(nrm, sacc);
+                }
+                x->wrn[l - 1] = nrm;
                 std::vector<uint16_t> f(C * C * 2), g(C * C * 2);
                 for (int w = 0; w < 4; ++w)
                     for (int kb = 0; kb < 8; ++kb)
@@ -744,6 +766,7 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
             a.zero = (const float*)x->zero;
             a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
             a.kd = x->kd[l]; a.kr = x->kr[l];
+            a.wrn = x->wrn[l];
             launch_block_bwd_s(a, s);
         } else if (x->bf) {
             // the bf16 chain holds d loss / d e_l with D_l already added (the kernel adds it)

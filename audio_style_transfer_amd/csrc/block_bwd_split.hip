@@ -8,17 +8,21 @@
 // fp32 storage, split fp16 operands on v_mfma_f32_32x32x16_f16, fp32 accumulation and
 // epilogue (splitwave.h).
 //
-// Per tile of 64 positions (one workgroup per CU, wave w owns channels 32 w .. 32 w + 31):
-//   top     wait for this tile's tot rows and mask words (DMA'd during the previous tile), B1;
-//           DMA this tile's D_l rows and the next tile's tot rows and mask words
-//   convert tot 2^m_t -> split image (m_t from the clip's max |tot|), B2
+// One workgroup per CU (wave w owns channels 32 w .. 32 w + 31), persistent over tiles of 64
+// positions.  A tile's tot rows are DMA'd into an LDS slot and converted there, in place, to
+// split tot (2^m_t, m_t from the clip's max |tot|) under the previous tile's step 2; two slots
+// alternate.  Per tile i:
+//   T       barrier
 //   step 1  g_v = W_r tot for the tile columns (+ the two halo rows of one-segment layouts),
-//           g_u = [u > 0] g_v, wave max -> LDS, B3; g_u 2^m_u -> split image, D_l landed, B4
-//   step 2  g_a = 3 taps x 8 k-blocks x 2 column tiles x 3 products
-//   epi     out = tot + [e_l > 0] g_a + D_l -> HBM (fp32); max |out| -> the clip's atomic max
-// Only DMA reads global memory (the compiler never waits on an in-flight DMA it cannot see);
-// every wave issues the same vector-memory sequence: D_l (9), next rows (9), masks (1), then
-// 8 row stores and 1 atomic.
+//           its 8 k-steps issuing tile i+1's tot-row and mask-word DMA; g_u = [u > 0] g_v 2^m_u
+//           -> split g_u image (m_u from the bound |g_v| <= wrn max|tot|: no cross-wave
+//           exchange), barrier
+//   step 2  g_a = 3 taps x 8 k-blocks x 2 column tiles x 3 products; steps 0..8 issue tile
+//           i's D_l DMA; after step 13: wait for tile i+1's rows + barrier, then steps 14..23
+//           carry their in-place conversion; D_l landed + barrier
+//   epi     out = tot (fp32, loaded before step 2) + [e_l > 0] g_a + D_l -> HBM; max |out|
+//           -> the clip's atomic max
+// Only DMA reads global memory (the compiler never waits on an in-flight DMA it cannot see).
 #include "splitwave.h"
 #include <algorithm>
 
@@ -29,10 +33,13 @@ using namespace sw;
 constexpr int MSLOT = 3 * 1024;   // mask words per tile (u16 index): u > 0 [64][8] at 0, e_l > 0
                                   // [64][8] at 512, halo u > 0 [2][8] at 1024
 
-// D_l rows: LDS row c = tile column c (64 rows, stride RS), 9 one-KiB groups per wave
+// D_l rows: LDS row c = tile column c (64 rows, stride RS), 9 one-KiB groups per wave; unmasked
+// layouts issue in the saddr form (tile base + a constant per-lane offset, rows past the tile
+// re-read column 0's row)
 template <bool MASKED>
 struct ColDma {
-    int soff[DPW], srow[DPW], schk[DPW];
+    uint32_t off[DPW];
+    int srow[DPW], schk[DPW];
     bool real[DPW];
     __device__ __forceinline__ void init(int w, int lane, const Layout& ly, int d) {
 #pragma unroll
@@ -42,19 +49,19 @@ struct ColDma {
             srow[j] = L;
             schk[j] = qc < 32 ? qc : 0;
             real[j] = L < TMS;
-            soff[j] = (MASKED || !real[j]) ? 0 : row_toff(frow(L, ly), ly, d) * C + schk[j] * 4;
+            off[j] = (MASKED || !real[j]) ? 0u : (uint32_t)((row_toff(frow(L, ly), ly, d) * C + schk[j] * 4) * 4);
         }
     }
     __device__ __forceinline__ void issue(int j, const float* src, const Tile& t, const float* zero,
                                           uint32_t lds0, int T, int n, int d) const {
+        if (!MASKED) {
+            dma16s(src + ((size_t)t.b * T + t.tb) * C, off[j], lds0 + j * 4096);
+            return;
+        }
         const float* p = zero;
         if (real[j]) {
-            if (MASKED) {
-                const int pp = t.p0 + srow[j];
-                p = src + ((size_t)t.b * T + (pp % n) * d + pp / n) * C + schk[j] * 4;
-            } else {
-                p = src + ((size_t)t.b * T + t.tb) * C + soff[j];
-            }
+            const int pp = t.p0 + srow[j];
+            p = src + ((size_t)t.b * T + (pp % n) * d + pp / n) * C + schk[j] * 4;
         }
         dma16(p, lds0 + j * 4096);
     }
@@ -62,18 +69,18 @@ struct ColDma {
 
 template <bool MASKED, bool ONESEG, bool HAS_D>
 __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
-    __shared__ __attribute__((aligned(16))) uint8_t XF[2][SLOT];    // fp32 tot rows
-    __shared__ __attribute__((aligned(16))) uint8_t XS[SLOT];       // split tot, then split g_u
+    __shared__ __attribute__((aligned(16))) uint8_t XS[2][SLOT];    // tot images (fp32 -> split)
+    __shared__ __attribute__((aligned(16))) uint8_t XG[SLOT];       // split g_u image
     __shared__ __attribute__((aligned(16))) uint8_t XD[SLOT];       // fp32 D_l rows (row = column)
     __shared__ __attribute__((aligned(16))) uint8_t MK[2][MSLOT];   // mask words
     __shared__ __attribute__((aligned(16))) uint8_t SCR[1024];      // wave 3's dummy mask group
-    __shared__ float RED[4];
 
     const int tiles = a.T / TMS;
     const int ntiles = a.B * tiles;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
+    const uint32_t padb = MASKED ? 0u : pad_bits(ly, w, lane);   // pad rows of the pairs converted
 
     auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, tiles, a.n, a.d, ly); };
     RowDma<MASKED> dma;
@@ -82,12 +89,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     if (HAS_D) ddma.init(w, lane, ly, a.d);
     // tot rows + mask words of tile tl into slot s: wave 0 the u > 0 words of the 64 columns,
     // wave 1 the e_l > 0 words, wave 2 the halo u > 0 words (lanes 0, 1), wave 3 a dummy group
-    auto issue_tile = [&](int tl, int s) {
-        const Tile t = tile_of(tl);
-        dma.aim(a.tin, t, ly, a.T, a.n);
-        const uint32_t lds0 = (uint32_t)(uintptr_t)&XF[s][0] + (uint32_t)(w * 1024);
-#pragma unroll
-        for (int j = 0; j < DPW; ++j) dma.issue(j, a.tin, a.zero, lds0, a.T, a.n, a.d);
+    auto issue_masks = [&](const Tile& t, int s) {
         const uint16_t* src = (const uint16_t*)a.zero;
         uint32_t dst = (uint32_t)(uintptr_t)&SCR[0];
         const size_t cb = (size_t)t.b * a.T;
@@ -100,7 +102,14 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         if (w < 3) dst = (uint32_t)(uintptr_t)&MK[s][w * 1024];
         dma16(src, dst);
     };
-    if (blockIdx.x < ntiles) issue_tile(blockIdx.x, 0);
+    if (blockIdx.x < ntiles) {
+        const Tile t = tile_of(blockIdx.x);
+        dma.aim(a.tin, t, ly, a.T, a.n, a.d);
+        const uint32_t lds0 = (uint32_t)(uintptr_t)&XS[0][0] + (uint32_t)(w * 1024);
+#pragma unroll
+        for (int j = 0; j < DPW; ++j) dma.issue(j, a.tin, a.zero, lds0, a.T, a.n, a.d);
+        issue_masks(t, 0);
+    }
 
     // this wave's split weight halves (A: rows = channels 32 w.., K = the other side's channels)
     uint4 wr[8][2], wd[3][8][2];
@@ -117,7 +126,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             for (int hl = 0; hl < 2; ++hl)
                 wd[tp][kb][hl] = a.wdb[((size_t)((w * 3 + tp) * 8 + kb) * 2 + hl) * 64 + lane];
     pin_all(wd, wr);
-    __syncthreads();
+    // the g_u image's pad / unused halo rows stay zero (only column and halo rows are written)
+    for (int i = tid; i < SLOT / 16; i += FT) reinterpret_cast<uint4*>(XG)[i] = make_uint4(0, 0, 0, 0);
 
     int Lc[2], toff[2];
 #pragma unroll
@@ -130,27 +140,42 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     // the halo column tile: lane r == 0 -> image row 0 (p0 - 1), r == 1 -> row 65 (p0 + 64)
     const int Lh = r == 1 ? TMS + 1 : 0;
 
+    if (blockIdx.x < ntiles) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        const Tile t0 = tile_of(blockIdx.x);
+        const float s0 = exp2i(scale_exp(sload(a.gmax_in + t0.b)));
+        const uint32_t z0 = zero_bits<MASKED>(padb, t0, ly, a.n, w, lane);
+#pragma unroll
+        for (int k = 0; k < NCONV; ++k) {
+            const int p = conv_pair(w, k);
+            pair_write<false>(&XS[0][0], p, pair_read(&XS[0][0], p, lane), conv_scale(z0, k, s0), lane);
+        }
+    }
+
     int it = 0;
     STAMP_DECL
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
         const int cur = it & 1;
         const Tile cu = tile_of(tile);
-        if (it) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (HAS_D) {
-            const uint32_t lds0 = (uint32_t)(uintptr_t)&XD[0] + (uint32_t)(w * 1024);
-#pragma unroll
-            for (int j = 0; j < DPW; ++j) ddma.issue(j, a.dadd, cu, a.zero, lds0, a.T, a.n, a.d);
-        }
-        issue_tile(tile + (int)gridDim.x < ntiles ? tile + (int)gridDim.x : ntiles - 1, cur ^ 1);
-
+        const int ntile = tile + (int)gridDim.x;
+        const bool has_next = ntile < ntiles;
+        // T: every wave is done with the previous tile (other slot, D rows, g_u image)
+        lds_barrier();
         STAMP(6)
-        const int m_t = scale_exp(sload(a.gmax_in + cu.b));
-        convert_rows<false>(&XF[cur][0], XS, ly.nrows, exp2i(m_t), w, lane);
-        lds_barrier();     // B2
-        STAMP(7)
+        const Tile nt = tile_of(has_next ? ntile : tile);
+        dma.aim(a.tin, nt, ly, a.T, a.n, a.d);
+        const uint32_t zn = zero_bits<MASKED>(padb, nt, ly, a.n, w, lane);
+        const uint32_t ldsn = (uint32_t)(uintptr_t)&XS[cur ^ 1][0] + (uint32_t)(w * 1024);
+        const uint32_t ldsd = (uint32_t)(uintptr_t)&XD[0] + (uint32_t)(w * 1024);
+
+        const float gm = sload(a.gmax_in + cu.b);
+        const int m_t = scale_exp(gm);
+        const int m_u = scale_exp(a.wrn * gm);
+        const float s_next = has_next ? exp2i(scale_exp(sload(a.gmax_in + nt.b))) : 0.f;
+        const uint8_t* xs = &XS[cur][0];
+        uint8_t* xn = &XS[cur ^ 1][0];
+        const uint16_t* mk = reinterpret_cast<const uint16_t*>(&MK[cur][0]);
 
         bool ok0[2] = {true, true}, ok2[2] = {true, true};
         if (MASKED) {
@@ -161,9 +186,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
                 ok2[j] = m < a.n - 1;
             }
         }
-        const uint16_t* mk = reinterpret_cast<const uint16_t*>(&MK[cur][0]);
 
-        // ---- step 1: g_v = W_r tot (columns, halo rows), g_u = [u > 0] g_v ----
+        // ---- step 1: g_v = W_r tot (columns, halo rows), g_u = [u > 0] g_v -> g_u image ----
         f32x16 acc[2], acch;
 #pragma unroll
         for (int i = 0; i < 16; ++i) { acc[0][i] = 0.f; acc[1][i] = 0.f; acch[i] = 0.f; }
@@ -172,7 +196,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             auto bload = [&](int kb, uint4 (&xh)[3], uint4 (&xl)[3]) {
 #pragma unroll
                 for (int j = 0; j < (ONESEG ? 3 : 2); ++j) {
-                    const uint8_t* p = XS + (j < 2 ? Lc[j] : Lh) * RS + kb * 32 + h * 16;
+                    const uint8_t* p = xs + (j < 2 ? Lc[j] : Lh) * RS + kb * 32 + h * 16;
                     xh[j] = lds16(p);
                     xl[j] = lds16(p + 256);
                 }
@@ -181,115 +205,136 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
 #pragma unroll
             for (int kb = 0; kb < 8; ++kb) {
                 const int cb = kb & 1;
+                // step order (step_schedule): first MFMA, DMA + next reads, the rest
+                acc[0] = mfma_f16(wr[kb][0], bh[cb][0], acc[0]);
+                // tile i+1's rows and mask words into the other slot (the last tile re-reads
+                // itself there: unused, and the count of vector-memory ops stays fixed)
+                dma.issue(kb, a.tin, a.zero, ldsn, a.T, a.n, a.d);
+                if (kb == 7) {
+                    dma.issue(8, a.tin, a.zero, ldsn, a.T, a.n, a.d);
+                    issue_masks(nt, cur ^ 1);
+                }
                 if (kb + 1 < 8) bload(kb + 1, bh[cb ^ 1], bl[cb ^ 1]);
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[j] = mfma3(wr[kb][0], wr[kb][1], bh[cb][j], bl[cb][j], acc[j]);
+                acc[0] = mfma_f16(wr[kb][1], bh[cb][0], acc[0]);
+                acc[0] = mfma_f16(wr[kb][0], bl[cb][0], acc[0]);
+                acc[1] = mfma3(wr[kb][0], wr[kb][1], bh[cb][1], bl[cb][1], acc[1]);
                 if (ONESEG) acch = mfma3(wr[kb][0], wr[kb][1], bh[cb][2], bl[cb][2], acch);
+                step_schedule();
             }
         }
-        float umax = 0.f;
         {
-            const float inv = exp2i(-(m_t + a.kr));
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                apply_mask(acc[j], mk[(32 * j + r) * 8 + 4 * h + w]);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    acc[j][i] *= inv;
-                    umax = fmaxf(umax, fabsf(acc[j][i]));
-                }
-            }
-            if (ONESEG) {
-                apply_mask(acch, mk[1024 + r * 8 + 4 * h + w]);   // lanes r >= 2: unused
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    acch[i] *= inv;
-                    if (r < 2) umax = fmaxf(umax, fabsf(acch[i]));
-                }
-            }
-            umax = wave_max(umax);
-            if (lane == 0) RED[w] = umax;
-        }
-        lds_barrier();     // B3: every wave is done with the tot image
-        float inv2;
-        {
-            const int m_u = scale_exp(fmaxf(fmaxf(RED[0], RED[1]), fmaxf(RED[2], RED[3])));
-            const float su = exp2i(m_u);
-            auto put = [&](const f32x16& v, int row) {
+            const float f = exp2i(m_u - m_t - a.kr);   // acc units 2^(m_t + k_r) -> g_u 2^m_u
+            auto put = [&](f32x16& v, int row) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     uint2 hi, lo;
-                    split4(v[4 * g] * su, v[4 * g + 1] * su, v[4 * g + 2] * su, v[4 * g + 3] * su, hi, lo);
-                    uint8_t* p = XS + row * RS + 2 * (chb + 8 * g);
+                    split4(v[4 * g] * f, v[4 * g + 1] * f, v[4 * g + 2] * f, v[4 * g + 3] * f, hi, lo);
+                    uint8_t* p = XG + row * RS + 2 * (chb + 8 * g);
                     *reinterpret_cast<uint2*>(p) = hi;
                     *reinterpret_cast<uint2*>(p + 256) = lo;
                 }
             };
 #pragma unroll
-            for (int j = 0; j < 2; ++j) put(acc[j], Lc[j]);
-            if (ONESEG && r < 2) put(acch, Lh);
-            // ---- step 2 (below) works in units of 2^(m_u + k_d) ----
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
-            inv2 = exp2i(-(m_u + a.kd));
+            for (int j = 0; j < 2; ++j) {
+                apply_mask(acc[j], mk[(32 * j + r) * 8 + 4 * h + w]);
+                put(acc[j], Lc[j]);
+            }
+            if (ONESEG) {
+                apply_mask(acch, mk[1024 + r * 8 + 4 * h + w]);   // lanes r >= 2: unused
+                if (r < 2) put(acch, Lh);
+            }
         }
-        // this wave's D_l rows have landed (younger: the next tile's 9 row groups + 1 mask group)
-        if (HAS_D) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-        lds_barrier();     // B4: g_u image complete (and every wave's D_l rows)
-        STAMP(8)
+        lds_barrier();     // g_u image complete
+        STAMP(7)
+        // tot in fp32 for the epilogue, this lane's accumulator elements (in flight during step 2)
+        float4 tv[2][4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const float* src = a.tin + ((size_t)cu.b * a.T + ctime(cu, 32 * j + r, toff[j])) * C + chb;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) tv[j][g] = *reinterpret_cast<const float4*>(src + 8 * g);
+        }
 
-        // ---- step 2: g_a = sum_k W_d[k] g_u(p - k + 1) ----
+        // ---- step 2: g_a = sum_k W_d[k] g_u(p - k + 1), next tile converted ----
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
         {
             uint4 bh[2][2], bl[2][2];
             auto bload = [&](int st, uint4 (&xh)[2], uint4 (&xl)[2]) {
                 const int tp = st >> 3, kb = st & 7;
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    const uint8_t* p = XS + (Lc[j] + 1 - tp) * RS + kb * 32 + h * 16;
+                    const uint8_t* p = XG + (Lc[j] + 1 - tp) * RS + kb * 32 + h * 16;
                     xh[j] = lds16(p);
                     xl[j] = lds16(p + 256);
+                    if (MASKED && ((tp == 0 && !ok2[j]) || (tp == 2 && !ok0[j]))) {
+                        xh[j] = make_uint4(0, 0, 0, 0);
+                        xl[j] = xh[j];
+                    }
                 }
             };
+            float4 cv[2];
             bload(0, bh[0], bl[0]);
 #pragma unroll
             for (int st = 0; st < 24; ++st) {
                 const int tp = st >> 3, kb = st & 7, cb = st & 1;
-                if (st + 1 < 24) bload(st + 1, bh[cb ^ 1], bl[cb ^ 1]);
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    uint4 xh = bh[cb][j], xl = bl[cb][j];
-                    if (MASKED && ((tp == 0 && !ok2[j]) || (tp == 2 && !ok0[j]))) {
-                        xh = make_uint4(0, 0, 0, 0);
-                        xl = xh;
-                    }
-                    acc[j] = mfma3(wd[tp][kb][0], wd[tp][kb][1], xh, xl, acc[j]);
+                if (st == 14) {
+                    // the next tile's rows / masks have landed (younger: the 8 tot loads and
+                    // this tile's 9 D_l groups; vmcnt retires in issue order)
+                    if (HAS_D) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    lds_barrier();
                 }
+                // step order (step_schedule): first MFMA; D_l DMA group, next reads (+ the
+                // conversion's pair read); the rest with the conversion of the pair read before
+                acc[0] = mfma_f16(wd[tp][kb][0], bh[cb][0], acc[0]);
+                if (HAS_D && st < DPW) ddma.issue(st, a.dadd, cu, a.zero, ldsd, a.T, a.n, a.d);
+                if (st + 1 < 24) bload(st + 1, bh[cb ^ 1], bl[cb ^ 1]);
+                if (st >= 14) {
+                    // row pair k = st - 14 read here, converted and written one step later (the
+                    // last tile converts its stale other slot: unused, branch-free)
+                    const int k = st - 14;
+                    if (k < NCONV) cv[k & 1] = pair_read(xn, conv_pair(w, k), lane);
+                    if (k > 0)
+                        pair_write<false>(xn, conv_pair(w, k - 1), cv[(k - 1) & 1],
+                                       conv_scale(zn, k - 1, s_next), lane);
+                }
+                acc[0] = mfma_f16(wd[tp][kb][1], bh[cb][0], acc[0]);
+                acc[0] = mfma_f16(wd[tp][kb][0], bl[cb][0], acc[0]);
+                acc[1] = mfma3(wd[tp][kb][0], wd[tp][kb][1], bh[cb][1], bl[cb][1], acc[1]);
+                step_schedule();
             }
         }
+        STAMP(8)
+        if (HAS_D) {   // this tile's D_l rows have landed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_barrier();
+        }
+#ifdef ASTYLE_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: + the tot loads' wait
+#endif
+        STAMP(12)
 
-        STAMP(9)
         // ---- epilogue: out = tot + [e_l > 0] g_a + D_l ----
         {
+            const float inv2 = exp2i(-(m_u + a.kd));
             float omax = 0.f;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int c = 32 * j + r;
                 apply_mask(acc[j], mk[512 + c * 8 + 4 * h + w]);
                 const int t = ctime(cu, c, toff[j]);
-                const uint8_t* tf = &XF[cur][0] + Lc[j] * RS + 4 * chb;
                 const uint8_t* df = XD + c * RS + 4 * chb;
                 float* dst = a.gout + ((size_t)cu.b * a.T + t) * C + chb;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const float4 tv = *reinterpret_cast<const float4*>(tf + 32 * g);
                     float4 o;
-                    o.x = fmaf(acc[j][4 * g + 0], inv2, tv.x);
-                    o.y = fmaf(acc[j][4 * g + 1], inv2, tv.y);
-                    o.z = fmaf(acc[j][4 * g + 2], inv2, tv.z);
-                    o.w = fmaf(acc[j][4 * g + 3], inv2, tv.w);
+                    o.x = fmaf(acc[j][4 * g + 0], inv2, tv[j][g].x);
+                    o.y = fmaf(acc[j][4 * g + 1], inv2, tv[j][g].y);
+                    o.z = fmaf(acc[j][4 * g + 2], inv2, tv[j][g].z);
+                    o.w = fmaf(acc[j][4 * g + 3], inv2, tv[j][g].w);
                     if (HAS_D) {
                         const float4 dv = *reinterpret_cast<const float4*>(df + 32 * g);
                         o.x += dv.x; o.y += dv.y; o.z += dv.z; o.w += dv.w;
@@ -301,7 +346,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             omax = wave_max(omax);
             if (lane == 0) atomicMax(a.gmax_out + cu.b, __float_as_uint(omax));
         }
-        STAMP(10)
+        STAMP(9)
     }
     STAMP_FLUSH(a.stamps)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

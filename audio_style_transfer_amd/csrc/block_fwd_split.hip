@@ -2,53 +2,70 @@
 //   u = dconv_d(relu(e_l)) + b_d        (masked.py:110-160, K = 3, SAME zero padding)
 //   e_{l+1} = e_l + W_r^T relu(u) + b_r
 // fp32 storage, v_mfma_f32_32x32x16_f16 on split fp16 operands, fp32 accumulation and fp32
-// epilogues (splitwave.h).  The residual e_l is added in fp32 from the tile's fp32 rows.
+// epilogues (splitwave.h).
 //
-// Per tile of 64 positions (one workgroup per CU, wave w owns output channels 32 w..32 w+31):
-//   top     wait for this tile's fp32 rows (DMA'd during the previous tile), barrier B1;
-//           store the previous tile's e_{l+1} > 0 words; DMA the next tile's rows
-//   convert relu(e_l) 2^m_e -> split image (m_e from the clip's max |e_l|), barrier B2
-//   GEMM 1  3 taps x 8 k-blocks x 2 column tiles x 3 products (A = W_d^T halves in AGPRs)
-//   epi 1   u = acc 2^-(m_e+k_d) + b_d, u > 0 words, v = relu(u), wave max -> LDS, B3;
-//           v 2^m_v -> split image (m_v from the tile's max v), u > 0 words -> HBM, B4
-//   GEMM 2  8 k-blocks x 2 column tiles x 3 products (A = W_r^T halves in AGPRs)
-//   epi 2   e_{l+1} = e_l + acc 2^-(m_v+k_r) + b_r -> HBM; e_{l+1} > 0 words (by the next
-//           layer's positions) staged in LDS; max |e_{l+1}| -> the clip's atomic max
-// Every wave issues the same vector-memory sequence after its DMA of the next tile (1 mask
-// store, 8 row stores, 1 atomic), so the top-of-tile wait is vmcnt(10).
+// One workgroup per CU (wave w owns output channels 32 w .. 32 w + 31), persistent over tiles
+// of 64 positions, one wave per SIMD: every epilogue runs in the shadow of MFMAs.  The two
+// 32-column halves j of a tile are separate MFMA phases, so the epilogue of one half overlaps
+// the GEMM of the other.  A tile's e_l arrives in registers a tile ahead, in rows (unit k:
+// image rows 8 k .. 8 k + 7 x wave w's 32 channels: 8 cache lines per wave instruction), and is
+// converted into the LDS image (split relu(e_l), scaled by 2^m_e from the clip's max |e_l|) and
+// into the wave's quarter of a residual buffer (fp32 e_l, double-buffered, read back by the
+// same wave only).  Per tile i:
+//   T  barrier (image i complete)
+//   A  GEMM 1, column half 0 (3 taps x 8 k-blocks x 3 products); carries epilogue 2 of tile
+//      i-1 (8 units of 3 steps: e_i = e_{i-1} + y + b_r -> HBM, e > 0 bits, max |e|)
+//   B  GEMM 1, column half 1; carries epilogue 1 of half 0 (u = acc 2^-(m_e+k_d) + b_d, u > 0
+//      bits, v = relu(u) 2^m_v -> split v image; m_v from the bound |u| <= wdn max|e_l| + bdm)
+//      barrier
+//   C  GEMM 2 (8 k-blocks x 3 products), half 0; carries epilogue 1 of half 1; barrier
+//   D  GEMM 2, half 1; carries the conversion of tile i+1 (image + residual) and, unit by
+//      unit behind it, the row loads of tile i+2
 #include "splitwave.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace ast {
 namespace {
 using namespace sw;
 
-template <bool MASKED>
+constexpr int IROWS = 72;             // image / residual rows: 66 or 68 used, 9 units x 8 rows
+constexpr int ISLOT = IROWS * RS;     // bytes per image / residual buffer
+constexpr int NU = 9;                 // row units per tile
+
+// one step of 3 MFMAs: the first, the next step's B reads, then the other two with side work
+__device__ __forceinline__ void step3_schedule() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // 1 MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);       // DS reads
+#pragma unroll
+    for (int m = 1; m < 3; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);   // VALU
+        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);   // DS writes
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool MASKED, bool ONESEG>
 __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
-    __shared__ __attribute__((aligned(16))) uint8_t XF[2][SLOT];   // fp32 e_l rows
-    __shared__ __attribute__((aligned(16))) uint8_t XS[SLOT];      // split relu(e_l), then split v
-    __shared__ __attribute__((aligned(16))) float BIAS[2 * C];     // b_d, b_r
-    __shared__ __attribute__((aligned(16))) uint16_t MBU[TMS * 8]; // u > 0 words of the tile
-    __shared__ __attribute__((aligned(16))) uint16_t MBE[TMS * 8]; // e_{l+1} > 0 words
-    __shared__ int MBT[TMS];                                       // time of each tile column
-    __shared__ float RED[4];
+    __shared__ __attribute__((aligned(16))) uint8_t IMG[ISLOT];     // split relu(e_l) image
+    __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];   // fp32 e_l (residual) rows
+    __shared__ __attribute__((aligned(16))) uint8_t XV[TMS * RS];   // split v image
+    __shared__ __attribute__((aligned(16))) float BIAS[2 * C];      // b_d, b_r
+    __shared__ __attribute__((aligned(16))) uint16_t MBU[TMS * 8];  // u > 0 words of the tile
+    __shared__ __attribute__((aligned(16))) uint16_t MBE[TMS * 8];  // e_{l+1} > 0 words
+    __shared__ int MBT[TMS];                                        // time of each tile column
 
     const int tiles = a.T / TMS;
     const int ntiles = a.B * tiles;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
+    const int G = (int)gridDim.x;
 
     auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, tiles, a.n, a.d, ly); };
-    RowDma<MASKED> dma;
-    dma.init(w, lane, ly, a.d);
-    auto issue_rows = [&](int tl, int slot) {
-        dma.aim(a.ein, tile_of(tl), ly, a.T, a.n);
-        const uint32_t lds0 = (uint32_t)(uintptr_t)&XF[slot][0] + (uint32_t)(w * 1024);
-#pragma unroll
-        for (int j = 0; j < DPW; ++j) dma.issue(j, a.ein, a.zero, lds0, a.T, a.n, a.d);
-    };
-    if (blockIdx.x < ntiles) issue_rows(blockIdx.x, 0);
+    // tiles past the end repeat the last one (loaded and converted, never used)
+    auto clampt = [&](int tl) { return tl < ntiles ? tl : ntiles - 1; };
 
     // this wave's split weight halves, resident in AGPRs for the whole launch: every load is
     // issued before the first pin (a pin right after its load would wait for it)
@@ -67,9 +84,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             wr[kb][hl] = a.wrf[((size_t)(w * 8 + kb) * 2 + hl) * 64 + lane];
     pin_all(wd, wr);
     if (tid < C) { BIAS[tid] = a.bd[tid]; BIAS[C + tid] = a.br[tid]; }
-    __syncthreads();
 
-    // this lane's two tile columns (32 j + r), their image rows and time offsets
     int Lc[2], toff[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -78,6 +93,63 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     }
     const int chb = 32 * w + 4 * h;   // first channel of this lane's accumulator group g = 0
     auto ctime = [&](const Tile& t, int cc, int to) { return col_time<MASKED>(t, cc, to, a.n, a.d); };
+
+    // ---- row units: unit k, lane -> image row L = 8 k + lr, channels cq .. cq + 3 ----
+    const int lr = lane >> 3;
+    const int cq = 32 * w + 4 * (lane & 7);
+    const uint32_t imgo = (uint32_t)(lr * RS + 2 * cq);   // + 8 k RS: split row bytes
+    const uint32_t ero = (uint32_t)(lr * RS + 4 * cq);    // + 8 k RS: fp32 row bytes
+    // unmasked layouts: byte offset of the unit's source row from the tile's row-0 source
+    // (time tb - d); rows without a source (pad rows, rows past the image) read row 1 and are
+    // zeroed (bit k of padz); one-segment halos (unit 0 row 0, unit 8 row 65) are decided per tile
+    uint32_t soff[NU];
+    uint32_t padz = 0;
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+        const int L = 8 * k + lr;
+        const bool none = MASKED ? (L == 0 || L > TMS) : (L >= ly.nrows || pad_row(L, ly));
+        if (none) padz |= 1u << k;
+        soff[k] = MASKED ? 0u : (uint32_t)(((none ? 0 : row_toff(L, ly, a.d)) + a.d) * C * 4 + 4 * cq);
+    }
+    const uint32_t row1 = (uint32_t)(a.d * C * 4 + 4 * cq), row64 = (uint32_t)((TMS * a.d + a.d) * C * 4 + 4 * cq);
+
+    float4 ld[NU];          // rows of the next tile to convert
+    auto load_unit = [&](const Tile& t, int k) {
+        if (MASKED) {
+            const int L = 8 * k + lr;
+            const int pp = t.p0 + ((padz >> k) & 1u ? 0 : L - 1);
+            const float* src = a.ein + ((size_t)t.b * a.T + (pp % a.n) * a.d + pp / a.n) * C + cq;
+            ld[k] = *reinterpret_cast<const float4*>(src);
+            return;
+        }
+        const char* base = reinterpret_cast<const char*>(a.ein + ((ptrdiff_t)t.b * a.T + t.tb - a.d) * C);
+        uint32_t o = soff[k];
+        if (ONESEG && k == 0 && lr == 0 && t.p0 % a.n == 0) o = row1;
+        if (ONESEG && k == NU - 1 && lr == 1 && t.p0 % a.n + TMS >= a.n) o = row64;
+        ld[k] = *reinterpret_cast<const float4*>(base + o);
+    };
+    auto zero_bits_of = [&](const Tile& t) {
+        uint32_t z = padz;
+        if (ONESEG) {
+            const int m0 = t.p0 % a.n;
+            if (lr == 0 && m0 == 0) z |= 1u;
+            if (lr == 1 && m0 + TMS >= a.n) z |= 1u << (NU - 1);
+        }
+        return z;
+    };
+    // conversion of unit k: raw fp32 -> residual buffer er; relu, scale, split -> image
+    auto conv_unit = [&](int k, uint8_t* er, float s, uint32_t zb) {
+        float4 v = ld[k];
+        *reinterpret_cast<float4*>(er + ero + 8 * k * RS) = v;
+        const float sk = (zb >> k) & 1u ? 0.f : s;
+        v.x = __int_as_float(max(__float_as_int(v.x), 0)); v.y = __int_as_float(max(__float_as_int(v.y), 0));
+        v.z = __int_as_float(max(__float_as_int(v.z), 0)); v.w = __int_as_float(max(__float_as_int(v.w), 0));
+        uint2 hi, lo;
+        split4(v.x * sk, v.y * sk, v.z * sk, v.w * sk, hi, lo);
+        uint8_t* p = IMG + imgo + 8 * k * RS;
+        *reinterpret_cast<uint2*>(p) = hi;
+        *reinterpret_cast<uint2*>(p + 256) = lo;
+    };
 
     // e_{l+1} > 0 words of a finished tile -> next layer's positions (wave w: columns 16 w..)
     auto store_me = [&](int b) {
@@ -90,182 +162,237 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         }
     };
 
-    int it = 0, prevb = 0;
-    STAMP_DECL
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
-        const int cur = it & 1;
-        const Tile cu = tile_of(tile);
-        // this wave's part of the tile's rows has landed (vmcnt retires in issue order; 10
-        // memory ops of the previous tile follow its DMA), the barrier publishes all parts
-        if (it) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (it) store_me(prevb);
-        issue_rows(tile + (int)gridDim.x < ntiles ? tile + (int)gridDim.x : ntiles - 1, cur ^ 1);
-
-        STAMP(0)
-        const int m_e = scale_exp(sload(a.gmax_in + cu.b));
-        convert_rows<true>(&XF[cur][0], XS, ly.nrows, exp2i(m_e), w, lane);
-        lds_barrier();     // B2: split image complete
-        STAMP(1)
-
-        bool ok0[2] = {true, true}, ok2[2] = {true, true};
-        if (MASKED) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int m = (cu.p0 + 32 * j + r) % a.n;
-                ok0[j] = m > 0;
-                ok2[j] = m < a.n - 1;
-            }
-        }
-
-        // ---- GEMM 1: u = sum_tap W_d[tap]^T relu(e_l)(p + tap - 1) ----
-        f32x16 acc[2];
+    // ---- epilogue 2 of tile prv (residual rows erp), unit u = (j, g) in three parts ----
+    f32x16 acc2[2];                    // y of the pending epilogue 2
+    Tile prv = tile_of(blockIdx.x);
+    float inv2p = 0.f;
+    float emax = 0.f;
+    uint32_t mb[2] = {0u, 0u};
+    float* dstj[2] = {nullptr, nullptr};
+    float4 e2e, e2b, e2o;
+    auto epi2_begin = [&]() {
+        emax = 0.f;
+        mb[0] = mb[1] = 0u;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
-        {
-            uint4 bh[2][2], bl[2][2];
-            auto bload = [&](int st, uint4 (&xh)[2], uint4 (&xl)[2]) {
-                const int tp = st >> 3, kb = st & 7;
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const uint8_t* p = XS + (Lc[j] + tp - 1) * RS + kb * 32 + h * 16;
-                    xh[j] = lds16(p);
-                    xl[j] = lds16(p + 256);
-                }
-            };
-            bload(0, bh[0], bl[0]);
-#pragma unroll
-            for (int st = 0; st < 24; ++st) {
-                const int tp = st >> 3, kb = st & 7, cb = st & 1;
-                if (st + 1 < 24) bload(st + 1, bh[cb ^ 1], bl[cb ^ 1]);
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    uint4 xh = bh[cb][j], xl = bl[cb][j];
-                    if (MASKED && ((tp == 0 && !ok0[j]) || (tp == 2 && !ok2[j]))) {
-                        xh = make_uint4(0, 0, 0, 0);
-                        xl = xh;
-                    }
-                    acc[j] = mfma3(wd[tp][kb][0], wd[tp][kb][1], xh, xl, acc[j]);
-                }
-            }
+            dstj[j] = a.eout + ((size_t)prv.b * a.T + ctime(prv, 32 * j + r, toff[j])) * C + chb;
+    };
+    auto epi2_part = [&](int u, int part, const uint8_t* erp) {
+        const int j = u >> 2, g = u & 3;
+        if (part == 0) {
+            e2e = *reinterpret_cast<const float4*>(erp + Lc[j] * RS + 4 * (chb + 8 * g));
+            e2b = *reinterpret_cast<const float4*>(&BIAS[C + chb + 8 * g]);
+        } else if (part == 1) {
+            e2o.x = e2e.x + fmaf(acc2[j][4 * g + 0], inv2p, e2b.x);
+            e2o.y = e2e.y + fmaf(acc2[j][4 * g + 1], inv2p, e2b.y);
+            e2o.z = e2e.z + fmaf(acc2[j][4 * g + 2], inv2p, e2b.z);
+            e2o.w = e2e.w + fmaf(acc2[j][4 * g + 3], inv2p, e2b.w);
+#if !(defined(SW_EXP) && SW_EXP == 8)
+            *reinterpret_cast<float4*>(dstj[j] + 8 * g) = e2o;
+#endif
+        } else {
+            emax = fmaxf(emax, fmaxf(fmaxf(fabsf(e2o.x), fabsf(e2o.y)), fmaxf(fabsf(e2o.z), fabsf(e2o.w))));
+            // bit mbit(4 g + q) = 4 q + g of the column's word (common.h)
+            mb[j] |= (e2o.x > 0.f ? 1u : 0u) << g | (e2o.y > 0.f ? 1u : 0u) << (4 + g) |
+                     (e2o.z > 0.f ? 1u : 0u) << (8 + g) | (e2o.w > 0.f ? 1u : 0u) << (12 + g);
         }
+    };
+    // words and column times to LDS (all lanes write: identical values per column)
+    auto epi2_words = [&]() {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int c = 32 * j + r;
+            MBE[c * 8 + 4 * h + w] = (uint16_t)mb[j];
+            MBT[c] = ctime(prv, c, toff[j]);
+        }
+    };
+    auto epi2_max = [&]() {
+        const float m = wave_max(emax);
+        if (lane == 0) atomicMax(a.gmax_out + prv.b, __float_as_uint(m));
+    };
 
-        STAMP(2)
-        // ---- epilogue 1: u, u > 0 words, v = relu(u) ----
-        {
-            const float inv1 = exp2i(-(m_e + a.kd));
-            float vmax = 0.f;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float4 b4 = *reinterpret_cast<const float4*>(&BIAS[chb + 8 * g]);
-                    acc[j][4 * g + 0] = fmaf(acc[j][4 * g + 0], inv1, b4.x);
-                    acc[j][4 * g + 1] = fmaf(acc[j][4 * g + 1], inv1, b4.y);
-                    acc[j][4 * g + 2] = fmaf(acc[j][4 * g + 2], inv1, b4.z);
-                    acc[j][4 * g + 3] = fmaf(acc[j][4 * g + 3], inv1, b4.w);
-                }
-                MBU[(32 * j + r) * 8 + 4 * h + w] = (uint16_t)mask_bits(acc[j]);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    acc[j][i] = fmaxf(acc[j][i], 0.f);
-                    vmax = fmaxf(vmax, acc[j][i]);
-                }
+    // ---- epilogue 1 of column half j, unit g in two parts: u, bits; v -> split v image ----
+    f32x16 acc1[2];
+    float inv1 = 0.f, sv = 0.f;
+    uint32_t mu_w = 0;
+    float4 e1u;
+    auto epi1_part = [&](int j, int g, int part) {
+        if (part == 0) {
+            const float4 b4 = *reinterpret_cast<const float4*>(&BIAS[chb + 8 * g]);
+            e1u.x = fmaf(acc1[j][4 * g + 0], inv1, b4.x);
+            e1u.y = fmaf(acc1[j][4 * g + 1], inv1, b4.y);
+            e1u.z = fmaf(acc1[j][4 * g + 2], inv1, b4.z);
+            e1u.w = fmaf(acc1[j][4 * g + 3], inv1, b4.w);
+            mu_w |= (e1u.x > 0.f ? 1u : 0u) << g | (e1u.y > 0.f ? 1u : 0u) << (4 + g) |
+                    (e1u.z > 0.f ? 1u : 0u) << (8 + g) | (e1u.w > 0.f ? 1u : 0u) << (12 + g);
+        } else {
+            uint2 hi, lo;
+            split4(fmaxf(e1u.x, 0.f) * sv, fmaxf(e1u.y, 0.f) * sv, fmaxf(e1u.z, 0.f) * sv,
+                   fmaxf(e1u.w, 0.f) * sv, hi, lo);
+            uint8_t* p = XV + (32 * j + r) * RS + 2 * (chb + 8 * g);
+            *reinterpret_cast<uint2*>(p) = hi;
+            *reinterpret_cast<uint2*>(p + 256) = lo;
+            if (g == 3) {
+                MBU[(32 * j + r) * 8 + 4 * h + w] = (uint16_t)mu_w;
+                mu_w = 0;
             }
-            vmax = wave_max(vmax);
-            if (lane == 0) RED[w] = vmax;
         }
-        lds_barrier();     // B3: every wave is done with the relu(e_l) image
-        const int m_v = scale_exp(fmaxf(fmaxf(RED[0], RED[1]), fmaxf(RED[2], RED[3])));
-        {
-            const float sv = exp2i(m_v);
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    uint2 hi, lo;
-                    split4(acc[j][4 * g] * sv, acc[j][4 * g + 1] * sv, acc[j][4 * g + 2] * sv,
-                           acc[j][4 * g + 3] * sv, hi, lo);
-                    uint8_t* p = XS + (32 * j + r) * RS + 2 * (chb + 8 * g);
-                    *reinterpret_cast<uint2*>(p) = hi;
-                    *reinterpret_cast<uint2*>(p + 256) = lo;
-                }
+    };
+
+    // ---- GEMM 1 of column half J over the image; side work per step ----
+    auto gemm1h = [&](auto j_tag, auto side, const Tile& cu) {
+        constexpr int J = decltype(j_tag)::value;
+        bool ok0 = true, ok2 = true;
+        if (MASKED) {
+            const int m = (cu.p0 + 32 * J + r) % a.n;
+            ok0 = m > 0;
+            ok2 = m < a.n - 1;
         }
-        // u > 0 words of the tile (this layer's positions): wave w stores columns 16 w .. +15
-        if (lane < 16)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc1[J][i] = 0.f;
+        uint4 bh[2], bl[2];
+        auto bread = [&](int st, uint4& xh, uint4& xl) {
+            const int tp = st >> 3, kb = st & 7;
+            const uint8_t* p = IMG + (Lc[J] + tp - 1) * RS + kb * 32 + h * 16;
+            xh = lds16(p);
+            xl = lds16(p + 256);
+        };
+        bread(0, bh[0], bl[0]);
+#pragma unroll
+        for (int st = 0; st < 24; ++st) {
+            const int tp = st >> 3, kb = st & 7, cb = st & 1;
+            uint4 xh = bh[cb], xl = bl[cb];
+            if (MASKED && ((tp == 0 && !ok0) || (tp == 2 && !ok2))) {
+                xh = make_uint4(0, 0, 0, 0);
+                xl = xh;
+            }
+            acc1[J] = mfma_f16(wd[tp][kb][0], xh, acc1[J]);
+            if (st + 1 < 24) bread(st + 1, bh[cb ^ 1], bl[cb ^ 1]);
+            side(st);
+            acc1[J] = mfma_f16(wd[tp][kb][1], xh, acc1[J]);
+            acc1[J] = mfma_f16(wd[tp][kb][0], xl, acc1[J]);
+            step3_schedule();
+        }
+    };
+    // ---- GEMM 2 of column half J over the v image ----
+    auto gemm2h = [&](auto j_tag, auto side) {
+        constexpr int J = decltype(j_tag)::value;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc2[J][i] = 0.f;
+        uint4 bh[2], bl[2];
+        auto bload = [&](int kb, uint4& xh, uint4& xl) {
+            const uint8_t* p = XV + (32 * J + r) * RS + kb * 32 + h * 16;
+            xh = lds16(p);
+            xl = lds16(p + 256);
+        };
+        bload(0, bh[0], bl[0]);
+#pragma unroll
+        for (int kb = 0; kb < 8; ++kb) {
+            const int cb = kb & 1;
+            acc2[J] = mfma_f16(wr[kb][0], bh[cb], acc2[J]);
+            if (kb + 1 < 8) bload(kb + 1, bh[cb ^ 1], bl[cb ^ 1]);
+            side(kb);
+            acc2[J] = mfma_f16(wr[kb][1], bh[cb], acc2[J]);
+            acc2[J] = mfma_f16(wr[kb][0], bl[cb], acc2[J]);
+            step3_schedule();
+        }
+    };
+    using J0 = std::integral_constant<int, 0>;
+    using J1 = std::integral_constant<int, 1>;
+
+    if (blockIdx.x >= ntiles) return;   // (grid = min(tiles, CUs): not taken)
+
+    // prologue: the first tile's image and residual rows; the second tile's rows in flight
+    {
+        const Tile t0 = tile_of(blockIdx.x);
+#pragma unroll
+        for (int k = 0; k < NU; ++k) load_unit(t0, k);
+        const uint32_t z0 = zero_bits_of(t0);
+        const float s0 = exp2i(scale_exp(sload(a.gmax_in + t0.b)));
+#pragma unroll
+        for (int k = 0; k < NU; ++k) conv_unit(k, &ER[0][0], s0, z0);
+        const Tile t1 = tile_of(clampt(blockIdx.x + G));
+#pragma unroll
+        for (int k = 0; k < NU; ++k) load_unit(t1, k);
+    }
+
+    STAMP_DECL
+    // one tile; FIRST (the peeled first tile) has no pending epilogue 2.  Peeling keeps the
+    // sequence of vector-memory operations identical in every loop iteration, so the compiler's
+    // counted waits for the row loads never include the epilogue's stores.
+    auto tile_body = [&](auto first_tag, int tile, int it) {
+        constexpr bool FIRST = decltype(first_tag)::value;
+        const Tile cu = tile_of(tile);
+        const Tile nt = tile_of(clampt(tile + G));
+        const Tile n2 = tile_of(clampt(tile + 2 * G));
+        // T: the image of this tile complete (converted during the previous phase D)
+        lds_barrier();
+        STAMP(0)
+        const float gm = sload(a.gmax_in + cu.b);
+        const int m_e = scale_exp(gm);
+        const int m_v = scale_exp(fmaf(a.wdn, gm, a.bdm));
+        const float s_next = exp2i(scale_exp(sload(a.gmax_in + nt.b)));
+        const uint32_t zn = zero_bits_of(nt);
+        inv1 = exp2i(-(m_e + a.kd));
+        sv = exp2i(m_v);
+        uint8_t* erp = &ER[(it & 1) ^ 1][0];   // the previous tile's residual, then the next's
+
+        // A: GEMM 1 half 0 + epilogue 2 of the previous tile
+        if (!FIRST) {
+            epi2_begin();
+            gemm1h(J0{}, [&](int st) { epi2_part(st / 3, st % 3, erp); }, cu);
+            epi2_words();
+            epi2_max();
+        } else {
+            gemm1h(J0{}, [&](int) {}, cu);
+        }
+        STAMP(5)
+        // B: GEMM 1 half 1 + epilogue 1 of half 0
+        gemm1h(J1{}, [&](int st) { if (st < 8) epi1_part(0, st >> 1, st & 1); }, cu);
+        lds_barrier();   // v image half 0, u > 0 words half 0, e > 0 words of tile i-1
+        STAMP(1)
+        if (!FIRST) store_me(prv.b);
+        // C: GEMM 2 half 0 + epilogue 1 of half 1
+        gemm2h(J0{}, [&](int kb) { epi1_part(1, kb >> 1, kb & 1); });
+        lds_barrier();   // v image half 1, all u > 0 words
+        STAMP(2)
+        if (lane < 16)   // u > 0 words of the tile (this layer's positions): wave w, columns 16 w..
             *reinterpret_cast<uint4*>(a.mu + ((size_t)cu.b * a.T + cu.p0 + 16 * w + lane) * 8) =
                 *reinterpret_cast<const uint4*>(&MBU[(16 * w + lane) * 8]);
-        lds_barrier();     // B4: v image complete
+        // D: GEMM 2 half 1 + conversion of tile i+1, each unit's registers reloaded with i+2
+        gemm2h(J1{}, [&](int kb) {
+            conv_unit(kb, erp, s_next, zn);
+#if !(defined(SW_EXP) && SW_EXP == 9)
+            load_unit(n2, kb);
+#endif
+            if (kb == 7) {
+                conv_unit(NU - 1, erp, s_next, zn);
+#if !(defined(SW_EXP) && SW_EXP == 9)
+                load_unit(n2, NU - 1);
+#endif
+            }
+        });
         STAMP(3)
-
-        // ---- GEMM 2: y = W_r^T v ----
+        prv = cu;
+        inv2p = exp2i(-(m_v + a.kr));
+    };
+    tile_body(std::true_type{}, (int)blockIdx.x, 0);
+    int it = 1;
+    for (int tile = (int)blockIdx.x + G; tile < ntiles; tile += G, ++it)
+        tile_body(std::false_type{}, tile, it);
+    // drain: epilogue 2 of the last tile
+    {
+        const uint8_t* erl = &ER[(it - 1) & 1][0];
+        epi2_begin();
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
-        {
-            uint4 bh[2][2], bl[2][2];
-            auto bload = [&](int kb, uint4 (&xh)[2], uint4 (&xl)[2]) {
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const uint8_t* p = XS + (32 * j + r) * RS + kb * 32 + h * 16;
-                    xh[j] = lds16(p);
-                    xl[j] = lds16(p + 256);
-                }
-            };
-            bload(0, bh[0], bl[0]);
-#pragma unroll
-            for (int kb = 0; kb < 8; ++kb) {
-                const int cb = kb & 1;
-                if (kb + 1 < 8) bload(kb + 1, bh[cb ^ 1], bl[cb ^ 1]);
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[j] = mfma3(wr[kb][0], wr[kb][1], bh[cb][j], bl[cb][j], acc[j]);
-            }
-        }
-
-        STAMP(4)
-        // ---- epilogue 2: e_{l+1} = e_l + y + b_r ----
-        {
-            const float inv2 = exp2i(-(m_v + a.kr));
-            float emax = 0.f;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int c = 32 * j + r;
-                const int t = ctime(cu, c, toff[j]);
-                const uint8_t* ef = &XF[cur][0] + Lc[j] * RS + 4 * chb;
-                float* dst = a.eout + ((size_t)cu.b * a.T + t) * C + chb;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float4 e = *reinterpret_cast<const float4*>(ef + 32 * g);
-                    const float4 b4 = *reinterpret_cast<const float4*>(&BIAS[C + chb + 8 * g]);
-                    float4 o;
-                    o.x = e.x + fmaf(acc[j][4 * g + 0], inv2, b4.x);
-                    o.y = e.y + fmaf(acc[j][4 * g + 1], inv2, b4.y);
-                    o.z = e.z + fmaf(acc[j][4 * g + 2], inv2, b4.z);
-                    o.w = e.w + fmaf(acc[j][4 * g + 3], inv2, b4.w);
-                    *reinterpret_cast<float4*>(dst + 8 * g) = o;
-                    acc[j][4 * g + 0] = o.x; acc[j][4 * g + 1] = o.y;
-                    acc[j][4 * g + 2] = o.z; acc[j][4 * g + 3] = o.w;
-                    emax = fmaxf(emax, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
-                }
-                MBE[c * 8 + 4 * h + w] = (uint16_t)mask_bits(acc[j]);
-                if (w == 0 && h == 0) MBT[c] = t;
-            }
-            emax = wave_max(emax);
-            if (lane == 0) atomicMax(a.gmax_out + cu.b, __float_as_uint(emax));
-        }
-        prevb = cu.b;
-        STAMP(5)
+        for (int st = 0; st < 24; ++st) epi2_part(st / 3, st % 3, erl);
+        epi2_words();
+        epi2_max();
+        lds_barrier();
+        store_me(prv.b);
     }
+    STAMP(4)
     STAMP_FLUSH(a.stamps)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (it) store_me(prevb);
 }
 
 }  // namespace
@@ -274,8 +401,10 @@ void launch_block_fwd_s(const FwdArgsS& a, hipStream_t s) {
     const int nt = a.B * (a.T / TMS);
     const dim3 grid(std::min(nt, sw::num_cus()));
     Layout ly;
-    if (pick_layout(a.n, ly)) hipLaunchKernelGGL(k_block_fwd_s<true>, grid, dim3(FT), 0, s, a, ly);
-    else hipLaunchKernelGGL(k_block_fwd_s<false>, grid, dim3(FT), 0, s, a, ly);
+    const bool masked = pick_layout(a.n, ly);
+    if (masked) hipLaunchKernelGGL((k_block_fwd_s<true, false>), grid, dim3(FT), 0, s, a, ly);
+    else if (ly.M == TMS) hipLaunchKernelGGL((k_block_fwd_s<false, true>), grid, dim3(FT), 0, s, a, ly);
+    else hipLaunchKernelGGL((k_block_fwd_s<false, false>), grid, dim3(FT), 0, s, a, ly);
 }
 
 int sw::num_cus() {

@@ -40,9 +40,9 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 // Diagnostic phase stamps (guide: In-kernel stamps).  Only -DASTYLE_STAMPS builds execute
 // them; cycle deltas per phase are summed per wave and added to a.stamps[phase] at exit.
 #ifdef ASTYLE_STAMPS
-#define STAMP_DECL unsigned long long st_acc[12] = {}; unsigned long long st_prev = stamp_now();
+#define STAMP_DECL unsigned long long st_acc[16] = {}; unsigned long long st_prev = stamp_now();
 #define STAMP(k) { const unsigned long long st_t = stamp_now(); st_acc[k] += st_t - st_prev; st_prev = st_t; }
-#define STAMP_FLUSH(ptr) if (((threadIdx.x & 63) == 0) && (ptr)) { for (int k = 0; k < 12; ++k) atomicAdd(&(ptr)[k], st_acc[k]); }
+#define STAMP_FLUSH(ptr) if (((threadIdx.x & 63) == 0) && (ptr)) { for (int k = 0; k < 16; ++k) atomicAdd(&(ptr)[k], st_acc[k]); }
 __device__ __forceinline__ unsigned long long stamp_now() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
@@ -173,6 +173,7 @@ struct FwdArgsS {
     int B, T, d, n;        // dilation, n = T / d
     int dn_log2, nn;       // next layer: log2 dilation, T / dilation
     int kd, kr;            // weight exponents
+    float wdn, bdm;        // max_co sum_{tap,ci} |W_d|, max |b_d|: |u| <= wdn max|e_l| + bdm
 };
 
 struct BwdArgsS {
@@ -187,6 +188,7 @@ struct BwdArgsS {
     const float* zero;
     int B, T, d, n;
     int kd, kr;
+    float wrn;             // max_ci sum_co |W_r|: |W_r tot| <= wrn max|tot|
 };
 
 struct GramArgs {

@@ -35,10 +35,11 @@ constexpr int FT = 256;                  // threads: one wave per SIMD
 constexpr int TMS = 64;                  // positions per tile
 constexpr int RS = 528;                  // LDS row stride (bytes): 512 + 16, conflict-free
                                          // column reads (row r starts at bank 4 r)
-constexpr int SLOT = 36864;              // bytes per LDS slot: up to 68 rows + DMA tail
 constexpr int DPW = 9;                   // one-KiB DMA groups per wave per slot (36 groups)
-static_assert(4 * DPW * 1024 == SLOT, "DMA groups tile the slot");
-static_assert(68 * RS <= SLOT, "slot holds the largest layout");
+constexpr int SLOT = 36992;              // bytes per LDS slot: 70 rows (the conversion's pairs
+                                         // 0..34), the DMA fills the first 36 KiB
+static_assert(4 * DPW * 1024 <= SLOT && 68 * RS <= 4 * DPW * 1024, "DMA groups cover every image row");
+static_assert(70 * RS <= SLOT, "the conversion's last pair stays inside the slot");
 
 struct Layout {            // uniform per launch (pick_layout)
     int M;                 // segment length; TMS = one segment with two halo rows
@@ -103,59 +104,124 @@ __device__ __forceinline__ void dma16(const void* src, uint32_t lds_base) {
                  : "=&s"(keep) : "v"(src), "s"(lds_base) : "memory");
 }
 
+// the same in the saddr form: address = base (uniform, scalar pair) + off (per lane, bytes)
+__device__ __forceinline__ void dma16s(const void* base, uint32_t off, uint32_t lds_base) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(off), "s"(base), "s"(lds_base) : "memory");
+}
+
+// Image rows of a tile with no source row are zeroed at conversion (unmasked layouts): the pad
+// rows of the segment layouts, and the halo rows of a one-segment tile at a sub-sequence end.
+// Their DMA reads a row of the same tile instead, so every DMA address is in bounds.
+__device__ __forceinline__ bool pad_row(int L, const Layout& ly) {
+    if (ly.M == TMS) return false;
+    const int k = L % (ly.M + 2);
+    return k == 0 || k == ly.M + 1;
+}
+// Conversion of a slot: wave w converts row pairs conv_pair(w, k) = min(w + 4 k, 34), k < 9
+// (pair 34 = rows 68, 69 lies past every image, inside the slot: converted twice, harmlessly,
+// by waves 2 and 3).
+// Lane bit k of the zero-row word: this lane's row 2 conv_pair(w, k) + (lane >> 5) is zeroed.
+constexpr int NCONV = 9;
+__device__ __forceinline__ int conv_pair(int w, int k) { return min(w + 4 * k, 34); }
+__device__ __forceinline__ uint32_t pad_bits(const Layout& ly, int w, int lane) {   // per launch
+    uint32_t z = 0;
+    for (int k = 0; k < NCONV; ++k)
+        if (pad_row(2 * conv_pair(w, k) + (lane >> 5), ly)) z |= 1u << k;
+    return z;
+}
+template <bool MASKED>
+__device__ __forceinline__ uint32_t zero_bits(uint32_t pad, const Tile& t, const Layout& ly, int n,
+                                              int w, int lane) {
+    if (MASKED || ly.M != TMS || w != 0) return MASKED ? 0u : pad;
+    const int m0 = t.p0 % n;
+    const int h = lane >> 5;
+    // row 0 = pair 0 (k 0) low half, row 65 = pair 32 (k 8) high half, both wave 0
+    return (h == 0 && m0 == 0 ? 1u : 0u) | (h == 1 && m0 + TMS >= n ? 1u << 8 : 0u);
+}
+__device__ __forceinline__ float conv_scale(uint32_t zb, int k, float s) {
+    return (zb >> k) & 1u ? 0.f : s;
+}
+
 // One wave's share of a slot: group g = w + 4 j (j < DPW) covers slot bytes [1024 g, +1024);
 // this lane's 16 B land at row L, chunk qc (qc == 32 is the row's pad chunk, filled with a
-// harmless re-read of chunk 0; rows >= nrows read the zero line).
+// harmless re-read of chunk 0).
+//   unmasked layouts: a constant byte offset per lane from the tile's row-0 source address
+//     (time tb - d; row_toff(L) + d >= 0), one saddr issue per group and no vector ALU.  Rows
+//     without a source read row 1 (pad rows, rows past the image) or the nearest tile row (a halo
+//     row at a sub-sequence end: rows 0 / 65 sit in groups 0 / 33, 34 = j 0 / DPW - 1) and are
+//     zeroed at conversion (ZeroRows).
+//   masked layouts (n < 32): gathered per lane, rows without a source read the zero line.
 template <bool MASKED>
-struct RowDma {
-    int soff[DPW];       // source element offset from the tile's base row (unmasked layouts)
-    int scls[DPW];       // source class: 0 row, 1 zero, 2 left halo, 3 right halo
-    int srow[DPW], schk[DPW];
+struct RowDma;
+
+template <>
+struct RowDma<false> {
+    uint32_t off[DPW];
+    uint32_t halt[2];    // j = 0 / DPW - 1: offset used when the lane's halo row has no source
+    int hcls[2];         // 0, or 2 (row 0) / 3 (row 65) of a one-segment layout
     const float* base;   // per tile (aim)
-    uint32_t vmask;      // classes with a real source row
-    Tile t;
+    bool lok, rok;
 
     __device__ __forceinline__ void init(int w, int lane, const Layout& ly, int d) {
 #pragma unroll
         for (int j = 0; j < DPW; ++j) {
-            const int g = w + 4 * j;
-            const int o = g * 1024 + lane * 16;
+            const int o = (w + 4 * j) * 1024 + lane * 16;
             const int L = o / RS, qc = (o - L * RS) >> 4;
             const int ch = qc < 32 ? qc : 0;
-            srow[j] = L;
-            schk[j] = ch;
-            int cls = 0;
-            if (L >= ly.nrows) cls = 1;
-            else if (ly.M == TMS) cls = L == 0 ? 2 : (L == TMS + 1 ? 3 : 0);
-            else {
-                const int k = L % (ly.M + 2);
-                cls = (k == 0 || k == ly.M + 1) ? 1 : 0;
+            const int Ls = (L >= ly.nrows || pad_row(L, ly)) ? 1 : L;
+            off[j] = (uint32_t)((row_toff(Ls, ly, d) + d) * C * 4 + ch * 16);
+            if (j == 0 || j == DPW - 1) {
+                const int q = j == 0 ? 0 : 1;
+                hcls[q] = ly.M == TMS && L == 0 ? 2 : (ly.M == TMS && L == TMS + 1 ? 3 : 0);
+                halt[q] = (uint32_t)((row_toff(L == 0 ? 1 : TMS, ly, d) + d) * C * 4 + ch * 16);
             }
-            if (MASKED && (L == 0 || L == TMS + 1)) cls = 1;   // no halo rows in masked layouts
-            scls[j] = cls;
-            soff[j] = MASKED || cls == 1 ? 0 : row_toff(L, ly, d) * C + ch * 4;
         }
+        lok = rok = true;
     }
-    // point the slots at tile nt of src ([B][T][C] fp32)
-    __device__ __forceinline__ void aim(const float* src, const Tile& nt, const Layout& ly, int T, int n) {
-        t = nt;
-        vmask = 1u;
-        if (!MASKED && ly.M == TMS) {
+    __device__ __forceinline__ void aim(const float* src, const Tile& nt, const Layout& ly, int T, int n, int d) {
+        if (ly.M == TMS) {
             const int m0 = nt.p0 % n;
-            vmask |= (m0 > 0 ? 4u : 0u) | (m0 + TMS < n ? 8u : 0u);
+            lok = m0 > 0;
+            rok = m0 + TMS < n;
         }
-        base = src + ((size_t)nt.b * T + nt.tb) * C;
+        base = src + ((ptrdiff_t)nt.b * T + nt.tb - d) * C;
     }
+    __device__ __forceinline__ void issue(int j, const float*, const float*, uint32_t lds0, int, int, int) const {
+        uint32_t o = off[j];
+        if (j == 0 || j == DPW - 1) {
+            const int q = j == 0 ? 0 : 1;
+            if ((hcls[q] == 2 && !lok) || (hcls[q] == 3 && !rok)) o = halt[q];
+        }
+        dma16s(base, o, lds0 + j * 4096);
+    }
+};
+
+template <>
+struct RowDma<true> {
+    int srow[DPW], schk[DPW];
+    bool zl[DPW];        // rows without a source (0, 65 and past the image)
+    Tile t;
+
+    __device__ __forceinline__ void init(int w, int lane, const Layout& ly, int) {
+#pragma unroll
+        for (int j = 0; j < DPW; ++j) {
+            const int o = (w + 4 * j) * 1024 + lane * 16;
+            const int L = o / RS, qc = (o - L * RS) >> 4;
+            srow[j] = L;
+            schk[j] = qc < 32 ? qc : 0;
+            zl[j] = L >= ly.nrows || L == 0 || L == TMS + 1;
+        }
+    }
+    __device__ __forceinline__ void aim(const float*, const Tile& nt, const Layout&, int, int, int) { t = nt; }
     __device__ __forceinline__ void issue(int j, const float* src, const float* zero, uint32_t lds0,
                                           int T, int n, int d) const {
         const float* p = zero;
-        if (MASKED) {
-            const int pp = t.p0 + srow[j] - 1;
-            if (scls[j] != 1 && pp >= 0 && pp < T)
-                p = src + ((size_t)t.b * T + (pp % n) * d + pp / n) * C + schk[j] * 4;
-        } else if ((vmask >> scls[j]) & 1u) {
-            p = base + soff[j];
-        }
+        const int pp = t.p0 + srow[j] - 1;
+        if (!zl[j] && pp >= 0 && pp < T)
+            p = src + ((size_t)t.b * T + (pp % n) * d + pp / n) * C + schk[j] * 4;
         dma16(p, lds0 + j * 4096);
     }
 };
@@ -178,22 +244,25 @@ __device__ __forceinline__ void split4(float a0, float a1, float a2, float a3, u
     lo = make_uint2(__builtin_bit_cast(uint32_t, l01), __builtin_bit_cast(uint32_t, l23));
 }
 
-// fp32 rows [0, nrows) of slot src -> split rows of dst (hi: bytes 0..255, lo: 256..511 of the
-// row), scaled by s (optionally relu'd first).  Two rows per wave instruction.
+// In-place conversion of one row pair of an LDS slot: fp32 rows 2 p, 2 p + 1 (as DMA'd) ->
+// split rows (hi: bytes 0..255, lo: 256..511) of s x (relu(x) with RELU).  One wave
+// instruction reads both rows whole before the same wave overwrites them, so the conversion is
+// safe in place.  pair_read / pair_write are the two halves, for software-pipelined conversion.
+__device__ __forceinline__ float4 pair_read(const uint8_t* slot, int p, int lane) {
+    return *reinterpret_cast<const float4*>(slot + (2 * p + (lane >> 5)) * RS + (lane & 31) * 16);
+}
 template <bool RELU>
-__device__ __forceinline__ void convert_rows(const uint8_t* src, uint8_t* dst, int nrows, float s,
-                                             int w, int lane) {
-    const int half = lane >> 5, l = lane & 31;
-    for (int pr = w; 2 * pr < nrows; pr += 4) {
-        const int row = 2 * pr + half;
-        const float4 v = *reinterpret_cast<const float4*>(src + row * RS + l * 16);
-        float a0 = v.x, a1 = v.y, a2 = v.z, a3 = v.w;
-        if (RELU) { a0 = fmaxf(a0, 0.f); a1 = fmaxf(a1, 0.f); a2 = fmaxf(a2, 0.f); a3 = fmaxf(a3, 0.f); }
-        uint2 hi, lo;
-        split4(a0 * s, a1 * s, a2 * s, a3 * s, hi, lo);
-        *reinterpret_cast<uint2*>(dst + row * RS + l * 8) = hi;
-        *reinterpret_cast<uint2*>(dst + row * RS + 256 + l * 8) = lo;
+__device__ __forceinline__ void pair_write(uint8_t* slot, int p, float4 v, float s, int lane) {
+    uint8_t* row = slot + (2 * p + (lane >> 5)) * RS;
+    const int l = lane & 31;
+    if (RELU) {   // relu as an integer max of the bits (negative floats are negative ints)
+        v.x = __int_as_float(max(__float_as_int(v.x), 0)); v.y = __int_as_float(max(__float_as_int(v.y), 0));
+        v.z = __int_as_float(max(__float_as_int(v.z), 0)); v.w = __int_as_float(max(__float_as_int(v.w), 0));
     }
+    uint2 hi, lo;
+    split4(v.x * s, v.y * s, v.z * s, v.w * s, hi, lo);
+    *reinterpret_cast<uint2*>(row + l * 8) = hi;
+    *reinterpret_cast<uint2*>(row + 256 + l * 8) = lo;
 }
 
 __device__ __forceinline__ f32x16 mfma_f16(uint4 a, uint4 b, f32x16 c) {
@@ -240,6 +309,24 @@ __device__ __forceinline__ void pin_all(uint4 (&wd)[3][8][2], uint4 (&wr)[8][2])
     for (int kb = 0; kb < 8; ++kb)
 #pragma unroll
         for (int hl = 0; hl < 2; ++hl) wr[kb][hl] = to_agpr(wr[kb][hl]);
+}
+
+// Instruction order of one GEMM k-step (6 MFMAs): the first MFMA (its B fragments were read a
+// step earlier), then the next step's LDS reads, then each remaining MFMA followed by a group of
+// vector ALU / LDS-write side work that issues in its shadow.  Side work that consumes an LDS
+// read issued a step earlier (the in-place conversion) then waits only for that read: LDS
+// counters retire in order, so work placed after this step's reads would also wait for them.
+// The step ends with a scheduling barrier.
+__device__ __forceinline__ void step_schedule() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // 1 MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);       // DS reads
+#pragma unroll
+    for (int m = 1; m < 6; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);   // up to 6 VALU
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // up to 1 DS write
+    }
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 __device__ __forceinline__ float wave_max(float v) {

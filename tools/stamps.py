@@ -20,7 +20,7 @@ if mode == 'bwd':
     eng.set_targets(torch.randn(T, 128) * 0.1, torch.randn(*eng.style_shape) * 0.01)
 run = (lambda: eng.loss_grad(x)) if mode == 'bwd' else (lambda: eng.forward(x))
 run(); torch.cuda.synchronize()
-buf = torch.zeros(12, dtype=torch.int64, device='cuda')
+buf = torch.zeros(16, dtype=torch.int64, device='cuda')
 lib = _lib.load()
 lib.ast_debug_stamps.argtypes = [ctypes.c_void_p]
 lib.ast_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
@@ -34,12 +34,19 @@ if prec == 'bf16':
     tiles = B * T // 128 * 30 / 256   # tiles per CU over the 30 block launches
     groups = ((0, 4), (4, 8))
 else:
-    names = ['fwd: top wait + B1 + DMA issue', 'fwd: convert + B2', 'fwd: GEMM1',
-             'fwd: epi1 + B3 + v + B4', 'fwd: GEMM2', 'fwd: epi2 (+stores)',
-             'bwd: top wait + B1 + DMA issue', 'bwd: convert + B2', 'bwd: step 1 + g_u + B3 + B4',
-             'bwd: step 2', 'bwd: epilogue (+stores)', '-']
+    names = {0: 'fwd: T barrier', 5: 'fwd: A GEMM1 half 0 + epi2(prev)',
+             1: 'fwd: B GEMM1 half 1 + epi1 half 0 + barrier', 2: 'fwd: C GEMM2 half 0 + epi1 half 1 + barrier',
+             3: 'fwd: D GEMM2 half 1 + convert + loads', 4: 'fwd: drain',
+             6: 'bwd: top barrier', 7: 'bwd: step 1 + DMA issue + g_u image + barrier',
+             8: 'bwd: step 2 + D DMA + convert', 12: 'bwd: D + tot loads wait',
+             9: 'bwd: epilogue (+stores)'}
     tiles = B * T // 64 * 30 / 256
-    groups = ((0, 6), (6, 11))
+    for grp in ((0, 5, 1, 2, 3, 4), (6, 7, 8, 12, 9)):
+        tot = sum(v[k] for k in grp)
+        for k in grp:
+            if v[k]:
+                print('%-48s %6.1f %%   %8.0f cycles/tile/wave' % (names[k], 100.0 * v[k] / tot, v[k] / (4 * 256 * tiles)))
+    sys.exit(0)
 for lo, hi in groups:
     tot = sum(v[lo:hi])
     for n, c in zip(names[lo:hi], v[lo:hi]):
