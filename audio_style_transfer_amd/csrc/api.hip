@@ -120,7 +120,7 @@ struct ast_ctx {
     float2* stft_tw = nullptr;              // STFT regulariser: twiddles [1024]
     float* stft_fpart = nullptr;            //   per-frame partial sums [B][nf]
     float* stft_gfr = nullptr;              //   per-frame gradients [B][nf][1024]
-    int lb_m = 0;                           // L-BFGS-B history size of the last ast_lbfgs_begin
+    bool lb_begun = false;                  // some workspace was started (ast_lbfgs_begin)
     void* zero = nullptr;                   // 256 zero bytes
     size_t gpart_elems = 0, smat_elems = 0; // per context (mode-dependent)
     int ncpart = 0;
@@ -841,9 +841,9 @@ int ast_lbfgs_begin(ast_ctx* x, void* ws, float* xd, const double* x0, const int
     if (!x || !ws || !xd) return fail(AST_E_ARG, "null argument");
     if (m < 1 || m > 32) return fail(AST_E_ARG, "L-BFGS-B history m must be in 1..32");
     if (maxiter < 1 || maxls < 1) return fail(AST_E_ARG, "maxiter and maxls must be >= 1");
-    if (!x0 && x->lb_m != m)
-        return fail(AST_E_STATE, "continuing needs a workspace started with the same m (pass x0)");
-    x->lb_m = m;
+    if (!x0 && !x->lb_begun)
+        return fail(AST_E_STATE, "continuing (x0 NULL) needs a workspace started with x0");
+    x->lb_begun = true;
     launch_lbfgs_begin(ws, xd, x0, active, x->cfg.batch, x->cfg.T, m, maxiter, maxls, ftol, gtol,
                        S(stream));
     HIPCHK(hipGetLastError());
@@ -853,16 +853,16 @@ int ast_lbfgs_begin(ast_ctx* x, void* ws, float* xd, const double* x0, const int
 int ast_lbfgs_step(ast_ctx* x, void* ws, float* xd, const float* grad, const float* parts,
                    void* stream) {
     if (!x || !ws || !xd || !grad || !parts) return fail(AST_E_ARG, "null argument");
-    if (!x->lb_m) return fail(AST_E_STATE, "ast_lbfgs_begin has not been called");
-    launch_lbfgs_step(ws, xd, grad, parts, x->cfg.batch, x->cfg.T, x->lb_m, S(stream));
+    if (!x->lb_begun) return fail(AST_E_STATE, "ast_lbfgs_begin has not been called");
+    launch_lbfgs_step(ws, xd, grad, parts, x->cfg.batch, x->cfg.T, S(stream));
     HIPCHK(hipGetLastError());
     return 0;
 }
 
 int ast_lbfgs_state(ast_ctx* x, const void* ws, int* info, double* x64, void* stream) {
     if (!x || !ws || !info) return fail(AST_E_ARG, "null argument");
-    if (!x->lb_m) return fail(AST_E_STATE, "ast_lbfgs_begin has not been called");
-    launch_lbfgs_state(ws, info, x64, x->cfg.batch, x->cfg.T, x->lb_m, S(stream));
+    if (!x->lb_begun) return fail(AST_E_STATE, "ast_lbfgs_begin has not been called");
+    launch_lbfgs_state(ws, info, x64, x->cfg.batch, x->cfg.T, S(stream));
     HIPCHK(hipGetLastError());
     return 0;
 }

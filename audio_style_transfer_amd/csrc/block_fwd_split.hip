@@ -32,6 +32,7 @@ using namespace sw;
 constexpr int IROWS = 72;             // image / residual rows: 66 or 68 used, 9 units x 8 rows
 constexpr int ISLOT = IROWS * RS;     // bytes per image / residual buffer
 constexpr int NU = 9;                 // row units per tile
+constexpr int LA = 2;                 // B-fragment lookahead (steps)
 
 // one step of 3 MFMAs: the first, the next step's B reads, then the other two with side work
 __device__ __forceinline__ void step3_schedule() {
@@ -193,8 +194,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         } else {
             emax = fmaxf(emax, fmaxf(fmaxf(fabsf(e2o.x), fabsf(e2o.y)), fmaxf(fabsf(e2o.z), fabsf(e2o.w))));
             // bit mbit(4 g + q) = 4 q + g of the column's word (common.h)
-            mb[j] |= (e2o.x > 0.f ? 1u : 0u) << g | (e2o.y > 0.f ? 1u : 0u) << (4 + g) |
-                     (e2o.z > 0.f ? 1u : 0u) << (8 + g) | (e2o.w > 0.f ? 1u : 0u) << (12 + g);
+            mb[j] |= pos_bit(e2o.x) << g | pos_bit(e2o.y) << (4 + g) | pos_bit(e2o.z) << (8 + g) |
+                     pos_bit(e2o.w) << (12 + g);
         }
     };
     // words and column times to LDS (all lanes write: identical values per column)
@@ -223,8 +224,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             e1u.y = fmaf(acc1[j][4 * g + 1], inv1, b4.y);
             e1u.z = fmaf(acc1[j][4 * g + 2], inv1, b4.z);
             e1u.w = fmaf(acc1[j][4 * g + 3], inv1, b4.w);
-            mu_w |= (e1u.x > 0.f ? 1u : 0u) << g | (e1u.y > 0.f ? 1u : 0u) << (4 + g) |
-                    (e1u.z > 0.f ? 1u : 0u) << (8 + g) | (e1u.w > 0.f ? 1u : 0u) << (12 + g);
+            mu_w |= pos_bit(e1u.x) << g | pos_bit(e1u.y) << (4 + g) | pos_bit(e1u.z) << (8 + g) |
+                    pos_bit(e1u.w) << (12 + g);
         } else {
             uint2 hi, lo;
             split4(fmaxf(e1u.x, 0.f) * sv, fmaxf(e1u.y, 0.f) * sv, fmaxf(e1u.z, 0.f) * sv,
@@ -250,24 +251,27 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc1[J][i] = 0.f;
-        uint4 bh[2], bl[2];
+        // B fragments are read LA steps ahead (a step is only 3 MFMAs: one step ahead leaves
+        // the LDS latency exposed)
+        uint4 bh[LA + 1], bl[LA + 1];
         auto bread = [&](int st, uint4& xh, uint4& xl) {
             const int tp = st >> 3, kb = st & 7;
             const uint8_t* p = IMG + (Lc[J] + tp - 1) * RS + kb * 32 + h * 16;
             xh = lds16(p);
             xl = lds16(p + 256);
         };
-        bread(0, bh[0], bl[0]);
+#pragma unroll
+        for (int q = 0; q < LA; ++q) bread(q, bh[q], bl[q]);
 #pragma unroll
         for (int st = 0; st < 24; ++st) {
-            const int tp = st >> 3, kb = st & 7, cb = st & 1;
+            const int tp = st >> 3, kb = st & 7, cb = st % (LA + 1);
             uint4 xh = bh[cb], xl = bl[cb];
             if (MASKED && ((tp == 0 && !ok0) || (tp == 2 && !ok2))) {
                 xh = make_uint4(0, 0, 0, 0);
                 xl = xh;
             }
             acc1[J] = mfma_f16(wd[tp][kb][0], xh, acc1[J]);
-            if (st + 1 < 24) bread(st + 1, bh[cb ^ 1], bl[cb ^ 1]);
+            if (st + LA < 24) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
             side(st);
             acc1[J] = mfma_f16(wd[tp][kb][1], xh, acc1[J]);
             acc1[J] = mfma_f16(wd[tp][kb][0], xl, acc1[J]);
@@ -279,18 +283,19 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         constexpr int J = decltype(j_tag)::value;
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc2[J][i] = 0.f;
-        uint4 bh[2], bl[2];
+        uint4 bh[LA + 1], bl[LA + 1];
         auto bload = [&](int kb, uint4& xh, uint4& xl) {
             const uint8_t* p = XV + (32 * J + r) * RS + kb * 32 + h * 16;
             xh = lds16(p);
             xl = lds16(p + 256);
         };
-        bload(0, bh[0], bl[0]);
+#pragma unroll
+        for (int q = 0; q < LA; ++q) bload(q, bh[q], bl[q]);
 #pragma unroll
         for (int kb = 0; kb < 8; ++kb) {
-            const int cb = kb & 1;
+            const int cb = kb % (LA + 1);
             acc2[J] = mfma_f16(wr[kb][0], bh[cb], acc2[J]);
-            if (kb + 1 < 8) bload(kb + 1, bh[cb ^ 1], bl[cb ^ 1]);
+            if (kb + LA < 8) bload(kb + LA, bh[(kb + LA) % (LA + 1)], bl[(kb + LA) % (LA + 1)]);
             side(kb);
             acc2[J] = mfma_f16(wr[kb][1], bh[cb], acc2[J]);
             acc2[J] = mfma_f16(wr[kb][0], bl[cb], acc2[J]);
@@ -340,7 +345,11 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         // A: GEMM 1 half 0 + epilogue 2 of the previous tile
         if (!FIRST) {
             epi2_begin();
+#if defined(SW_EXP) && SW_EXP == 10
+            gemm1h(J0{}, [&](int) {}, cu);
+#else
             gemm1h(J0{}, [&](int st) { epi2_part(st / 3, st % 3, erp); }, cu);
+#endif
             epi2_words();
             epi2_max();
         } else {
@@ -348,7 +357,13 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         }
         STAMP(5)
         // B: GEMM 1 half 1 + epilogue 1 of half 0
+#if defined(SW_EXP) && SW_EXP == 10
+        gemm1h(J1{}, [&](int) {}, cu);
+#pragma unroll
+        for (int st = 0; st < 8; ++st) epi1_part(0, st >> 1, st & 1);
+#else
         gemm1h(J1{}, [&](int st) { if (st < 8) epi1_part(0, st >> 1, st & 1); }, cu);
+#endif
         lds_barrier();   // v image half 0, u > 0 words half 0, e > 0 words of tile i-1
         STAMP(1)
         if (!FIRST) store_me(prv.b);

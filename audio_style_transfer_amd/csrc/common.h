@@ -307,9 +307,8 @@ size_t lbfgs_workspace_bytes(int B, int T, int m);
 void launch_lbfgs_begin(void* ws, float* x, const double* x0, const int* active, int B, int T,
                         int m, int maxiter, int maxls, double tol, double pgtol, hipStream_t s);
 void launch_lbfgs_step(void* ws, float* x, const float* grad, const float* parts, int B, int T,
-                       int m, hipStream_t s);
-void launch_lbfgs_state(const void* ws, int* info, double* x64, int B, int T, int m,
-                        hipStream_t s);
+                       hipStream_t s);
+void launch_lbfgs_state(const void* ws, int* info, double* x64, int B, int T, hipStream_t s);
 
 void launch_adam(float* x, float* m, float* v, const float* g, size_t n, float lr, float b1,
                  float b2, float eps, float bc1, float bc2, hipStream_t s);

@@ -43,6 +43,14 @@ struct LbState {
 };
 static_assert(sizeof(LbState) <= 512, "LbState slot");
 
+// workspace header (first 512 B): the history size the workspace was laid out with, read by
+// every step / state launch, so a workspace can never be indexed with another loop's m
+struct LbHeader {
+    int magic, m, B, T;
+};
+constexpr int LB_MAGIC = 0x4c42464d;
+constexpr size_t LB_HDR = 512;
+
 // reasons (ast_lbfgs_state)
 enum { LB_RUNNING = 0, LB_STOP_ITER = 1, LB_CONV_PGTOL = 2, LB_CONV_REL_F = 3, LB_ABNORMAL = 4 };
 
@@ -64,7 +72,7 @@ struct Ws {   // workspace views for clip b
 
 __device__ __forceinline__ Ws ws_view(void* base, int B, int T, int m, int b) {
     Ws w;
-    char* p = (char*)base;
+    char* p = (char*)base + LB_HDR;
     w.st = (LbState*)p + b;
     double* v = (double*)(p + (size_t)B * 512);
     const size_t per = (size_t)(4 + 2 * m) * T;     // X0 X1 R D S[m] Y[m]
@@ -322,14 +330,16 @@ struct StepArgs {
     float* x;
     const float* grad;
     const float* parts;
-    int B, T, m;
+    int B, T;
 };
+
+__device__ __forceinline__ int ws_m(const void* ws) { return ((const LbHeader*)ws)->m; }
 
 __global__ void __launch_bounds__(NT) k_lbfgs_step(StepArgs a) {
     __shared__ double red[NT / 64];
     __shared__ double alpha[LB_MMAX];
     const int b = blockIdx.x, T = a.T;
-    const Ws w = ws_view(a.ws, a.B, T, a.m, b);
+    const Ws w = ws_view(a.ws, a.B, T, ws_m(a.ws), b);
     LbState s = *w.st;
     if (s.phase == 0) return;
     float* xd = a.x + (size_t)b * T;
@@ -425,8 +435,10 @@ __global__ void __launch_bounds__(NT) k_lbfgs_begin(void* ws, float* x, const do
                                                     int maxiter, int maxls, double tol,
                                                     double pgtol) {
     const int b = blockIdx.x;
+    if (!x0) m = ws_m(ws);   // a continuation keeps the workspace's own history size
     const Ws w = ws_view(ws, B, T, m, b);
     LbState s = *w.st;
+    if (x0 && b == 0 && threadIdx.x == 0) *(LbHeader*)ws = LbHeader{LB_MAGIC, m, B, T};
     if (x0) {
         for (int k = 0; k < (int)(sizeof(LbState) / 4); ++k) ((int*)&s)[k] = 0;
         const double* src = x0 + (size_t)b * T;
@@ -441,9 +453,9 @@ __global__ void __launch_bounds__(NT) k_lbfgs_begin(void* ws, float* x, const do
     if (threadIdx.x == 0) *w.st = s;
 }
 
-__global__ void k_lbfgs_state(const void* ws, int* info, double* x64, int B, int T, int m) {
+__global__ void k_lbfgs_state(const void* ws, int* info, double* x64, int B, int T) {
     const int b = blockIdx.x;
-    const Ws w = ws_view(const_cast<void*>(ws), B, T, m, b);
+    const Ws w = ws_view(const_cast<void*>(ws), B, T, ws_m(ws), b);
     const LbState& s = *w.st;
     if (threadIdx.x == 0) {
         info[b * 4 + 0] = s.phase;
@@ -460,7 +472,7 @@ __global__ void k_lbfgs_state(const void* ws, int* info, double* x64, int B, int
 }  // namespace
 
 size_t lbfgs_workspace_bytes(int B, int T, int m) {
-    return (size_t)B * 512 + (size_t)B * (4 + 2 * (size_t)m) * T * 8;
+    return LB_HDR + (size_t)B * 512 + (size_t)B * (4 + 2 * (size_t)m) * T * 8;
 }
 
 void launch_lbfgs_begin(void* ws, float* x, const double* x0, const int* active, int B, int T,
@@ -470,14 +482,13 @@ void launch_lbfgs_begin(void* ws, float* x, const double* x0, const int* active,
 }
 
 void launch_lbfgs_step(void* ws, float* x, const float* grad, const float* parts, int B, int T,
-                       int m, hipStream_t s) {
-    StepArgs a{ws, x, grad, parts, B, T, m};
+                       hipStream_t s) {
+    StepArgs a{ws, x, grad, parts, B, T};
     hipLaunchKernelGGL(k_lbfgs_step, dim3(B), dim3(NT), 0, s, a);
 }
 
-void launch_lbfgs_state(const void* ws, int* info, double* x64, int B, int T, int m,
-                        hipStream_t s) {
-    hipLaunchKernelGGL(k_lbfgs_state, dim3(B), dim3(256), 0, s, ws, info, x64, B, T, m);
+void launch_lbfgs_state(const void* ws, int* info, double* x64, int B, int T, hipStream_t s) {
+    hipLaunchKernelGGL(k_lbfgs_state, dim3(B), dim3(256), 0, s, ws, info, x64, B, T);
 }
 
 }  // namespace ast

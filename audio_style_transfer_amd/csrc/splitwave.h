@@ -335,6 +335,14 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// [x > 0] as 0 / 1 for every non-NaN x: the bits as a signed integer clamped to [0, 1] (one
+// v_med3_i32; +0 and negatives give 0)
+__device__ __forceinline__ uint32_t pos_bit(float x) {
+    uint32_t b;
+    asm("v_med3_i32 %0, %1, 0, 1" : "=v"(b) : "v"(x));
+    return b;
+}
+
 // relu-mask word of a lane's 32 x 32 accumulator tile: bit mbit(i) = acc[i] > 0 (the bf16
 // path's layout, common.h)
 __device__ __forceinline__ uint32_t mask_bits(const f32x16& acc) {

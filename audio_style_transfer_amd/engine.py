@@ -48,6 +48,7 @@ class StyleEngine:
         self.cnt_channels = int(cnt_channels)
         self.lambd = float(lambd)
         self.gamma = float(gamma)
+        self.gen = 0    # bumped by every setting a captured graph bakes in (set_gamma)
         cfg = _lib.AstCfg()
         cfg.batch, cfg.T = self.batch, self.T
         cfg.n_cont = len(self.cont_ids)
@@ -156,6 +157,7 @@ class StyleEngine:
         """The STFT regulariser weight (--gamma, methods.py:125)."""
         _lib.check(self.lib.ast_set_gamma(self.h, float(gamma)))
         self.gamma = float(gamma)
+        self.gen += 1   # captured graphs hold launch parameters derived from gamma: recapture
 
     def loss_grad(self, x: torch.Tensor, grad: Optional[torch.Tensor] = None,
                   parts: Optional[torch.Tensor] = None):
@@ -183,6 +185,15 @@ class StyleEngine:
                                               self._ptr(grad), self._ptr(step_dev, torch.int32), float(lr),
                                               float(beta1), float(beta2), float(eps),
                                               self._stream()))
+
+    @staticmethod
+    def nonfinite_clips(parts: torch.Tensor, grad: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Per-clip flag [B] (bool, on the device): the clip's loss parts or its gradient hold a
+        NaN / Inf (the reference would carry them into the next L-BFGS-B step)."""
+        bad = ~torch.isfinite(parts).all(dim=1)
+        if grad is not None:
+            bad |= ~torch.isfinite(grad).all(dim=1)
+        return bad
 
     def timing(self, enable: bool) -> None:
         _lib.check(self.lib.ast_timing(self.h, int(enable)))
@@ -215,18 +226,23 @@ class AdamLoop:
         self.hp = (float(lr), float(beta1), float(beta2), float(eps))
         self.graph = None
         if graph:
-            saved = [t.clone() for t in (self.x, self.m, self.v, self.step_dev)]
-            side = torch.cuda.Stream(device=x.device)
-            side.wait_stream(torch.cuda.current_stream(x.device))
-            with torch.cuda.stream(side):
-                self._eager()
-            torch.cuda.current_stream(x.device).wait_stream(side)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._eager()
-            for t, s in zip((self.x, self.m, self.v, self.step_dev), saved):
-                t.copy_(s)
-            self.graph = g
+            self._capture()
+
+    def _capture(self):
+        x = self.x
+        saved = [t.clone() for t in (self.x, self.m, self.v, self.step_dev)]
+        side = torch.cuda.Stream(device=x.device)
+        side.wait_stream(torch.cuda.current_stream(x.device))
+        with torch.cuda.stream(side):
+            self._eager()
+        torch.cuda.current_stream(x.device).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._eager()
+        for t, s in zip((self.x, self.m, self.v, self.step_dev), saved):
+            t.copy_(s)
+        self.graph = g
+        self._gen = self.eng.gen
 
     def _eager(self):
         self.eng.loss_grad(self.x, self.grad, self.parts)
@@ -234,6 +250,8 @@ class AdamLoop:
 
     def step(self):
         if self.graph is not None:
+            if self._gen != self.eng.gen:   # gamma changed since capture
+                self._capture()
             self.graph.replay()
         else:
             self._eager()
@@ -296,6 +314,8 @@ class LbfgsLoop:
 
     def step(self):
         if self.use_graph:
+            if self.graph is not None and self._gen != self.eng.gen:
+                self.graph = None           # gamma changed since capture: capture again
             if self.graph is None:
                 # captured at the first step after begin(): capture records the pair without
                 # executing it, and the state lives in ws, so every replay is an eager step
@@ -303,6 +323,7 @@ class LbfgsLoop:
                 with torch.cuda.graph(g):
                     self._eager()
                 self.graph = g
+                self._gen = self.eng.gen
             self.graph.replay()
         else:
             self._eager()

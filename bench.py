@@ -186,7 +186,8 @@ def run(args, Eng, precision, steps, warmup, ws, rank, dev, graph, clips=None, g
     el = time.perf_counter() - t0
     el = max_over_ranks(el, ws, device=dev)
     last_loss = loop.parts[:, 0].mean().item()
-    bad = int((~torch.isfinite(loop.parts[:, 0])).sum().item())   # per-clip non-finite flag
+    # per-clip flag: the clip's loss parts or gradient hold a NaN / Inf
+    bad = int((~torch.isfinite(loop.parts).all(dim=1) | ~torch.isfinite(loop.grad).all(dim=1)).sum().item())
     eng.timing(True)
     for _ in range(2):
         loop._eager()

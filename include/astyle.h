@@ -113,8 +113,10 @@ int ast_adam_step_dev(ast_ctx* ctx, float* x_dev, float* m_dev, float* v_dev, co
  *   ast_lbfgs_begin(x0)                       x_dev <- fp32(x0): the first point to evaluate
  *   repeat { ast_loss_grad(x_dev -> grad, parts); ast_lbfgs_step(grad, parts) -> next x_dev }
  *   until every clip's phase (ast_lbfgs_state) is 0
- * ws_dev: caller-owned device workspace of ast_lbfgs_workspace_bytes.  x0_dev [batch, T]
- * float64 (NULL: continue from each clip's current point, the next epoch of methods.py:164);
+ * ws_dev: caller-owned device workspace of ast_lbfgs_workspace_bytes(m); it records the m it
+ * was started with (begin with x0), and step / state / a continuation use that m, so loops of
+ * different m may share a context.  x0_dev [batch, T] float64 (NULL: continue from each clip's
+ * current point with the workspace's own m, the next epoch of methods.py:164);
  * active_dev [batch] int (NULL = all) selects the clips that run.  info_dev [batch, 4] =
  * (phase, iterations, evaluations, reason: 0 running, 1 maxiter, 2 pgtol, 3 rel. reduction
  * of f, 4 abnormal line search); x64_dev [batch, T] (may be NULL) the current float64 point.

@@ -65,3 +65,48 @@ def test_gatysnet_run_end_to_end(tmp_path, weights):
                                lambd=100.0, gamma=0.1, **kw)
     assert abs(h[0, 0] - parts[0]) <= 1e-4 * abs(parts[0]), (h[0], parts)
     assert abs(h[0, 3] - parts[3]) <= 1e-4 * abs(parts[3]) + 1e-9, (h[0], parts)
+
+
+def test_gatysnet_targets_and_output_wav(tmp_path, weights):
+    """methods.py:97-111,183-216: phi_c, and phi_s = l2norm(phi(content) + mean_<=5 phi(target
+    clips) - mean_<=5 phi(source clips)), as GatysNet.run builds them from wav files, against
+    oracle.targets_from_audio on the same samples; and ep-0.wav holds
+    inv_mu_law(x)[late:-late] / max (methods.py:169-176) of the returned point."""
+    from scipy.io import wavfile
+    from audio_style_transfer_amd import utils
+    from audio_style_transfer_amd.methods import GatysNet
+    sr, T = 16000, 4096
+    cont = synthetic_clips(1, 3 * sr, 1000)[0]
+    sty = synthetic_clips(1, 3 * sr, 5000)[0]
+    src = synthetic_clips(1, 3 * sr, 7000)[0]
+    cf, sf, rf = (str(tmp_path / n) for n in ('c.wav', 's.wav', 'r.wav'))
+    _write(cf, cont)
+    _write(sf, sty)
+    _write(rf, src)
+    out = tmp_path / 'out'
+    out.mkdir()
+    net = GatysNet(str(out), None, str(tmp_path / 'log'), str(tmp_path / 'fig'), stack=0,
+                   batch_size=T, cont_lyr_ids=[9], weights=weights, plots=False)
+    audio = net.run(cf, rf, sf, epochs=1, lambd=100.0, gamma=0.0)
+    # the oracle on the samples run() reads (same loader; start = 1 s, methods.py:195-200)
+    late = O.late_of(T)
+    a_c, _ = utils.load_audio(cf, sr=sr)
+    st = int(1.0 * sr - late)
+    clip = a_c[st:st + T]
+    a_s, _ = utils.load_audio(sf, sr=sr)
+    a_r, _ = utils.load_audio(rf, sr=sr)
+    clips = lambda a: [O.mu_law_numpy(a[i:i + T]) for i in range(0, min(len(a), 5 * T) - T + 1, T)]
+    kw = dict(cont_ids=[9], style_ids=list(range(10)), gatys=False, nb_channels=128,
+              cnt_channels=128)
+    phi_c, phi_s = O.targets_from_audio(weights, O.mu_law_numpy(clip), clips(a_s), clips(a_r), **kw)
+    got_c, got_s = (t.cpu().numpy().astype(np.float64) for t in net.engine._targets)
+    assert rel(got_c.reshape(phi_c.shape), phi_c) <= 1e-5
+    assert rel(got_s.reshape(phi_s.shape), phi_s) <= 1e-5
+    # ep-0.wav
+    fs, wav = wavfile.read(str(out / 'ep-0.wav'))
+    want = audio[late:-late] / np.max(audio[late:-late])
+    assert fs == sr and wav.dtype == np.float32 and wav.shape == want.shape
+    assert rel(wav, want) <= 1e-6
+    # ori.wav / style.wav are the content / target crops
+    _, ori = wavfile.read(str(out / 'ori.wav'))
+    assert rel(ori, clip[late:-late]) <= 1e-6

@@ -139,3 +139,51 @@ def test_device_lbfgs_epochs_and_inactive_clips(weights, dev):
     _, xb = loop.state(with_x=True)
     assert info[1, 2] == 0 and torch.equal(xa[1], xb[1])
     assert info[0, 2] > 0 and not torch.equal(xa[0], xb[0])
+
+
+def test_two_loops_of_different_m_share_an_engine(weights, dev):
+    """Each workspace keeps the m it was started with: a loop of m 3 interleaved
+    with a loop of m 10 on the same engine runs exactly as it does alone, and a continuation
+    (begin(None)) of either keeps its own m."""
+    from audio_style_transfer_amd.engine import LbfgsLoop
+    B, T = 2, 2048
+    eng, _, x0 = _setup(B, T, weights, dev)
+    alone = LbfgsLoop(eng, m=3, maxiter=6)
+    alone.minimize(torch.tensor(x0), check_every=1)
+    alone.minimize(None, check_every=1)
+    ref = alone.state(with_x=True)
+    a = LbfgsLoop(eng, m=3, maxiter=6)
+    b = LbfgsLoop(eng, m=10, maxiter=6)
+    a.begin(torch.tensor(x0))
+    b.begin(torch.tensor(x0))          # started last: the context's most recent m is 10
+    for _ in range(3):
+        a.step()
+        b.step()
+    while a.state()[0][:, 0].any():
+        a.step()
+    a.minimize(None, check_every=1)    # continuation of the m 3 workspace
+    got = a.state(with_x=True)
+    assert (got[0] == ref[0]).all()
+    assert torch.equal(got[1], ref[1])
+
+
+def test_gamma_change_after_capture_is_not_ignored(weights, dev):
+    """A captured step graph must follow set_gamma: graph replays with a gamma
+    change in between equal eager steps with the same change."""
+    from audio_style_transfer_amd.engine import AdamLoop
+    B, T = 2, 2048
+    eng, _, x0 = _setup(B, T, weights, dev)
+    outs = []
+    for graph in (False, True):
+        eng.set_gamma(0.0)
+        x = torch.tensor(x0, dtype=torch.float32, device=dev)
+        loop = AdamLoop(eng, x, lr=1.0, graph=graph)
+        for i in range(4):
+            if i == 2:
+                eng.set_gamma(0.5)
+            p = loop.step()
+        torch.cuda.synchronize()
+        outs.append((x.clone(), p.clone()))
+    assert float(outs[0][1][:, 3].abs().sum()) > 0        # the regulariser term is live
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
