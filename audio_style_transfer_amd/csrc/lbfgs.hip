@@ -444,6 +444,11 @@ __global__ void __launch_bounds__(NT) k_lbfgs_begin(void* ws, float* x, const do
         const double* src = x0 + (size_t)b * T;
         for (int i = threadIdx.x; i < T; i += NT) w.X[0][i] = src[i];
     }
+    if (!x0 && (!active || active[b])) {   // a new epoch starts from the float32 rounding of
+                                            // the point (the TF variable); idle clips keep theirs
+        double* X = w.X[s.xi];
+        for (int i = threadIdx.x; i < T; i += NT) X[i] = (double)(float)X[i];
+    }
     s.m = m; s.maxiter = maxiter; s.maxls = maxls; s.tol = tol; s.pgtol = pgtol;
     s.col = 0; s.head = 0; s.theta = 1.0; s.iter = 0; s.nfev = 0; s.ifun = 0;
     s.reason = LB_RUNNING;

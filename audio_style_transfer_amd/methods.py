@@ -35,6 +35,14 @@ def load_weights(path):
     return None
 
 
+def _drop_sess(args):
+    """The reference's methods take a tf.Session first (methods.py:86,97,140); drop it (None or
+    any object with a ``run`` method) so reference-style calls work unchanged."""
+    if args and (args[0] is None or hasattr(args[0], 'run')):
+        return args[1:]
+    return args
+
+
 class GatysNet(object):
     """methods.py:19-216, on one GPU; ``batch`` > 1 optimises independent clips together."""
 
@@ -75,17 +83,25 @@ class GatysNet(object):
                            gatys=self.gatys, lambd=lambd, precision=self.precision,
                            device=self.device, weights=self.weights)
 
-    def get_embeds(self, aud, is_content=True):
-        """methods.py:86-95: mu-law encode the clip and fetch embeds_c or embeds_s."""
-        aud = np.asarray(aud)
+    def get_embeds(self, *args, is_content=True):
+        """methods.py:86-95: mu-law encode the clip and fetch embeds_c or embeds_s.  Accepts the
+        reference's signature get_embeds(sess, aud) as well (the session is ignored)."""
+        aud = np.asarray(_drop_sess(args)[0])
         if aud.ndim == 1:
             aud = aud[:self.batch_size].reshape(1, self.batch_size)
         x = torch.tensor(utils.mu_law_numpy(aud), dtype=torch.float32, device=self.device)
         emb_c, emb_s = self.engine.embeds(x, content=is_content, style=not is_content)
         return (emb_c if is_content else emb_s)[0].cpu().numpy()
 
-    def get_style_phi(self, filename, max_examples=5, show_mat=True):
-        """methods.py:97-111: mean style embedding over <= 5 consecutive clips."""
+    def get_style_phi(self, *args, max_examples=5, show_mat=True):
+        """methods.py:97-111: mean style embedding over <= 5 consecutive clips.  Accepts the
+        reference's get_style_phi(sess, filename, ...) as well (the session is ignored)."""
+        args = _drop_sess(args)
+        filename = args[0]
+        if len(args) > 1:
+            max_examples = args[1]
+        if len(args) > 2:
+            show_mat = args[2]
         audio, _ = utils.load_audio(filename, sr=self.sr, audio_channel=0)
         I = []
         i = 0
@@ -97,11 +113,17 @@ class GatysNet(object):
             utils.show_gram(phi, figdir=self.figdir, gatys=self.gatys)
         return phi
 
-    def l_bfgs(self, phi_c, phi_s, epochs, lambd, gamma, x0=None, log=print, optimizer='scipy'):
+    def l_bfgs(self, *args, x0=None, log=print, optimizer='scipy', maxiter=100, **kw):
         """methods.py:140-181 with scipy L-BFGS-B driving ast_loss_grad (``optimizer='scipy'``,
         one host round trip per evaluation, as the reference), or the same L-BFGS-B run on the
-        device (``'device'``: ast_lbfgs_*, no round trip; progress is logged per epoch)."""
+        device (``'device'``: ast_lbfgs_*, no round trip; progress is logged per epoch).
+        Accepts the reference's l_bfgs(sess, phi_c, phi_s, epochs, lambd, gamma) as well.  Every
+        epoch starts from the float32 rounding of its point, as the TF variable does."""
         from scipy.optimize import minimize
+        names = ('phi_c', 'phi_s', 'epochs', 'lambd', 'gamma')
+        vals = dict(zip(names, _drop_sess(args)))
+        vals.update(kw)
+        phi_c, phi_s, epochs, lambd, gamma = (vals[n] for n in names)
         eng = self.build(self.batch_size, lambd=lambd) if lambd != self.engine.lambd else self.engine
         self.engine = eng
         eng.set_targets(torch.as_tensor(phi_c, dtype=torch.float32),
@@ -109,6 +131,7 @@ class GatysNet(object):
         eng.set_gamma(gamma)                                              # methods.py:121-125
         T = self.batch_size
         x = np.zeros(T) + 1e-6 if x0 is None else np.asarray(x0, dtype=np.float64)  # methods.py:49-54
+        x = x.astype(np.float32).astype(np.float64)       # the TF variable is float32
         xd = torch.empty(1, T, device=self.device)
         state = {'i': 0, 'i_': 0, 'since': time.time()}
         history = []
@@ -129,12 +152,12 @@ class GatysNet(object):
         loop = None
         if optimizer == 'device':
             from .engine import LbfgsLoop
-            loop = LbfgsLoop(eng, maxiter=100)
+            loop = LbfgsLoop(eng, maxiter=maxiter)
         for ep in range(epochs):
             state['ep'], state['i'] = ep, 0
             if loop is None:
-                res = minimize(fg, x, jac=True, method='L-BFGS-B', options={'maxiter': 100})
-                x = res.x
+                res = minimize(fg, x, jac=True, method='L-BFGS-B', options={'maxiter': maxiter})
+                x = res.x.astype(np.float32).astype(np.float64)   # next epoch: fp32(res.x)
             else:
                 info = loop.minimize(torch.tensor(x[None], dtype=torch.float64) if ep == 0 else None)
                 x = loop.state(with_x=True)[1][0].cpu().numpy()

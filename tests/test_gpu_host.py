@@ -110,3 +110,30 @@ def test_gatysnet_targets_and_output_wav(tmp_path, weights):
     # ori.wav / style.wav are the content / target crops
     _, ori = wavfile.read(str(out / 'ori.wav'))
     assert rel(ori, clip[late:-late]) <= 1e-6
+
+
+def test_gatysnet_device_optimizer_matches_scipy_path(tmp_path, weights):
+    """GatysNet.l_bfgs(optimizer='device') (ast_lbfgs_*) against the scipy path on the same HIP
+    loss: epochs=2 of maxiter 5 — the first epoch needs < 50 evaluations, so both stop after it
+    (methods.py:180-181) — the same point (the two differ only in fp64 reduction order), and
+    the reference's session-first call form.  Epoch continuation on the device is covered by
+    test_gpu_lbfgs.py::test_device_lbfgs_epochs_and_inactive_clips."""
+    from audio_style_transfer_amd.methods import GatysNet
+    T = 4096
+    out = tmp_path / 'out'
+    out.mkdir()
+    net = GatysNet(str(out), None, str(tmp_path / 'log'), str(tmp_path / 'fig'), stack=0,
+                   batch_size=T, cont_lyr_ids=[9], weights=weights, plots=False)
+    xc = O.mu_law_numpy(synthetic_clips(1, T, 1000)[0])
+    xs = O.mu_law_numpy(synthetic_clips(1, T, 5000)[0])
+    kw = dict(cont_ids=[9], style_ids=list(range(10)), gatys=False, nb_channels=128,
+              cnt_channels=128)
+    phi_c, phi_s = O.targets_from_audio(weights, xc, [xs], [xc], **kw)
+    logs = []
+    xa = net.l_bfgs(None, phi_c, phi_s, 2, 100.0, 0.0, optimizer='scipy', maxiter=5,
+                    log=logs.append)
+    xb = net.l_bfgs(phi_c, phi_s, epochs=2, lambd=100.0, gamma=0.0, optimizer='device',
+                    maxiter=5, log=logs.append)
+    assert os.path.isfile(out / 'ep-0.wav') and not os.path.isfile(out / 'ep-1.wav')
+    assert rel(xb, xa) <= 1e-6, rel(xb, xa)
+    assert np.array_equal(xa, xa.astype(np.float32).astype(np.float64))   # fp32-rounded epochs

@@ -120,3 +120,26 @@ def test_first_iterations_match_fp64_oracle(tag, T, precision, weights, dev):
                                         res_h.nfev, res_o.nfev))
     for e, v in zip(errs, envs):
         assert e <= max(BAR, 2.0 * v)
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'split'])
+def test_full_epoch_reaches_the_fp64_point(precision, weights, dev):
+    """One reference epoch (maxiter 100) of 'ours' at T=4096 converges (projected-gradient
+    test) to the fp64 oracle's point: final x within 1e-3 rel-L2 (measured 9e-5 fp32, 6e-5
+    split, 7e-5 for the torch fp32 reference; profiles/r2_trajectory_ours_T4096.json)."""
+    kw = CASES['ours']
+    T = 4096
+    x0 = np.full(T, np.float64(np.float32(1e-6)))
+    key = ('epoch', T)
+    if key not in _ORACLE:
+        phi_c, phi_s = _targets(kw, T, weights)
+        res_o, _ = _oracle_run(kw, T, weights, phi_c, phi_s, x0, 100)
+        _ORACLE[key] = (phi_c, phi_s, res_o)
+    phi_c, phi_s, res_o = _ORACLE[key]
+    res_h, _ = _hip_run(kw, T, weights, phi_c, phi_s, x0, 100, precision, dev)
+    e = float(np.linalg.norm(res_h.x - res_o.x) / np.linalg.norm(res_o.x))
+    print('epoch %s: x rel-L2 %.3g | it %d / %d | f %.7g / %.7g | %s' % (precision, e, res_h.nit,
+          res_o.nit, res_h.fun, res_o.fun, res_h.message))
+    assert res_h.nit < 100 and res_o.nit < 100          # both converged inside the epoch
+    assert e <= BAR
+    assert abs(res_h.fun - res_o.fun) <= 1e-4 * abs(res_o.fun)
