@@ -52,9 +52,14 @@ def main(tag, precision, clips, T):
     summary = {'tag': tag, 'precision': precision, 'clips': clips, 'T': T, 'kernels': stats}
     with open(os.path.join(dst, tag + '_summary.json'), 'w') as f:
         json.dump(summary, f, indent=1)
-    def pick(prefix):   # fp32 'k_block_fwd' or bf16 'k_block_fwd_bf16' (either layout variant)
-        ks = [k for k in stats if k.startswith(prefix) and 'hbm_bytes_per_launch' in stats[k]]
-        return max((stats[k] for k in ks), key=lambda v: v['calls'], default={})
+    def pick(name):   # every layout / template variant of the kernel, weighted by calls
+        ks = [k for k in stats if name in k and 'hbm_bytes_per_launch' in stats[k]]
+        n = sum(stats[k]['calls'] for k in ks)
+        if not n:
+            return {}
+        return {'hbm_bytes_per_launch': sum(stats[k]['hbm_bytes_per_launch'] * stats[k]['calls']
+                                            for k in ks) / n,
+                'avg_ms': sum(stats[k]['avg_ms'] * stats[k]['calls'] for k in ks) / n, 'calls': n}
     fw, bw = pick('k_block_fwd'), pick('k_block_bwd')
     if 'hbm_bytes_per_launch' in fw and 'hbm_bytes_per_launch' in bw:
         tj = {'precision': precision, 'clips': clips, 'T': T, 'source': tag,
@@ -64,8 +69,8 @@ def main(tag, precision, clips, T):
         with open(os.path.join(dst, 'traffic.json'), 'w') as f:
             json.dump(tj, f, indent=1)
     for k, v in sorted(stats.items(), key=lambda kv: -kv[1]['total_ms'])[:10]:
-        print('%-28s calls %4d avg %8.3f ms  hbm/launch %s' % (
-            k, v['calls'], v['avg_ms'],
+        print('%-60s calls %4d avg %8.3f ms  hbm/launch %s' % (
+            k[:60], v['calls'], v['avg_ms'],
             '%.3f GB (%.0f GB/s)' % (v['hbm_bytes_per_launch'] / 1e9, v['hbm_GBs'])
             if 'hbm_bytes_per_launch' in v else '-'))
 
