@@ -31,21 +31,7 @@ using namespace sw;
 
 constexpr int IROWS = 72;             // image / residual rows: 66 or 68 used, 9 units x 8 rows
 constexpr int ISLOT = IROWS * RS;     // bytes per image / residual buffer
-constexpr int NU = 9;                 // row units per tile
 constexpr int LA = 2;                 // B-fragment lookahead (steps)
-
-// one step of 3 MFMAs: the first, the next step's B reads, then the other two with side work
-__device__ __forceinline__ void step3_schedule() {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // 1 MFMA
-    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);       // DS reads
-#pragma unroll
-    for (int m = 1; m < 3; ++m) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);   // VALU
-        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);   // DS writes
-    }
-    __builtin_amdgcn_sched_barrier(0);
-}
 
 template <bool MASKED, bool ONESEG>
 __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
@@ -112,7 +98,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         if (none) padz |= 1u << k;
         soff[k] = MASKED ? 0u : (uint32_t)(((none ? 0 : row_toff(L, ly, a.d)) + a.d) * C * 4 + 4 * cq);
     }
-    const uint32_t row1 = (uint32_t)(a.d * C * 4 + 4 * cq), row64 = (uint32_t)((TMS * a.d + a.d) * C * 4 + 4 * cq);
+    const uint32_t row1 = (uint32_t)(a.d * C * 4 + 4 * cq), row64 = (uint32_t)(TMS * a.d * C * 4 + 4 * cq);   // image row 64 (time tb + 63 d)
 
     float4 ld[NU];          // rows of the next tile to convert
     auto load_unit = [&](const Tile& t, int k) {

@@ -145,6 +145,81 @@ __device__ __forceinline__ float conv_scale(uint32_t zb, int k, float s) {
     return (zb >> k) & 1u ? 0.f : s;
 }
 
+// ---- register-fed row units (block kernels): unit k (k < NU), lane -> image row
+//      L = 8 k + (lane >> 3), channels cq .. cq + 3 of the wave's quarter (32 w .. 32 w + 31):
+//      one wave instruction loads 8 rows x 128 B (8 cache lines).  Unmasked layouts address a
+//      unit as the tile's row-0 source (time tb - d) + a constant per-lane byte offset; rows
+//      without a source (pad rows, rows past the image, a one-segment halo at a sub-sequence
+//      end) read a row of the tile and are zeroed at conversion (zero bit k).  Masked layouts
+//      gather per lane (rows 0 and 65 have no source). ----
+constexpr int NU = 9;
+template <bool MASKED, bool ONESEG>
+struct RowUnits {
+    int lr, cq;
+    uint32_t imgo, ero;      // LDS byte offsets of the lane's split / fp32 chunk in row lr
+    uint32_t soff[NU];
+    uint32_t padz;
+    uint32_t row1, row64;
+
+    __device__ __forceinline__ void init(int w, int lane, const Layout& ly, int d) {
+        lr = lane >> 3;
+        cq = 32 * w + 4 * (lane & 7);
+        imgo = (uint32_t)(lr * RS + 2 * cq);
+        ero = (uint32_t)(lr * RS + 4 * cq);
+        padz = 0;
+#pragma unroll
+        for (int k = 0; k < NU; ++k) {
+            const int L = 8 * k + lr;
+            const bool none = MASKED ? (L == 0 || L > TMS) : (L >= ly.nrows || pad_row(L, ly));
+            if (none) padz |= 1u << k;
+            soff[k] = MASKED ? 0u : (uint32_t)(((none ? 0 : row_toff(L, ly, d)) + d) * C * 4 + 4 * cq);
+        }
+        row1 = (uint32_t)(d * C * 4 + 4 * cq);
+        row64 = (uint32_t)(TMS * d * C * 4 + 4 * cq);       // image row 64 (time tb + 63 d)
+    }
+    // unit k of tile t of tensor src ([B][T][C] fp32)
+    __device__ __forceinline__ float4 load(const float* src, const Tile& t, int k, int T, int n, int d) const {
+        if (MASKED) {
+            const int L = 8 * k + lr;
+            const int pp = t.p0 + ((padz >> k) & 1u ? 0 : L - 1);
+            return *reinterpret_cast<const float4*>(src + ((size_t)t.b * T + (pp % n) * d + pp / n) * C + cq);
+        }
+        const char* base = reinterpret_cast<const char*>(src + ((ptrdiff_t)t.b * T + t.tb - d) * C);
+        uint32_t o = soff[k];
+        if (ONESEG && k == 0 && lr == 0 && t.p0 % n == 0) o = row1;
+        if (ONESEG && k == NU - 1 && lr == 1 && t.p0 % n + TMS >= n) o = row64;
+        return *reinterpret_cast<const float4*>(base + o);
+    }
+    __device__ __forceinline__ uint32_t zero_bits(const Tile& t, int n) const {
+        uint32_t z = padz;
+        if (ONESEG) {
+            const int m0 = t.p0 % n;
+            if (lr == 0 && m0 == 0) z |= 1u;
+            if (lr == 1 && m0 + TMS >= n) z |= 1u << (NU - 1);
+        }
+        return z;
+    }
+};
+
+// x where bit k of word wd is set, else 0 (v_bfe_i32 + v_and)
+__device__ __forceinline__ float keep_if(float x, uint32_t wd, int k) {
+    const int s = ((int)(wd << (31 - k))) >> 31;
+    return __int_as_float(__float_as_int(x) & s);
+}
+
+// one step of 3 MFMAs: the first, the next step's B reads, then the other two with side work
+__device__ __forceinline__ void step3_schedule() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // 1 MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);       // DS reads
+#pragma unroll
+    for (int m = 1; m < 3; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);   // VALU
+        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);   // DS writes
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // One wave's share of a slot: group g = w + 4 j (j < DPW) covers slot bytes [1024 g, +1024);
 // this lane's 16 B land at row L, chunk qc (qc == 32 is the row's pad chunk, filled with a
 // harmless re-read of chunk 0).

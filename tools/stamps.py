@@ -37,11 +37,11 @@ else:
     names = {0: 'fwd: T barrier', 5: 'fwd: A GEMM1 half 0 + epi2(prev)',
              1: 'fwd: B GEMM1 half 1 + epi1 half 0 + barrier', 2: 'fwd: C GEMM2 half 0 + epi1 half 1 + barrier',
              3: 'fwd: D GEMM2 half 1 + convert + loads', 4: 'fwd: drain',
-             6: 'bwd: top barrier', 7: 'bwd: step 1 + DMA issue + g_u image + barrier',
-             8: 'bwd: step 2 + D DMA + convert', 12: 'bwd: D + tot loads wait',
-             9: 'bwd: epilogue (+stores)'}
+             6: 'bwd: T barrier', 7: 'bwd: A/B/H g_v + g_u + epi half 1 (prev) + barrier',
+             8: 'bwd: C g_a half 0 + convert + loads', 9: 'bwd: D g_a half 1 + epi half 0',
+             12: 'bwd: drain'}
     tiles = B * T // 64 * 30 / 256
-    for grp in ((0, 5, 1, 2, 3, 4), (6, 7, 8, 12, 9)):
+    for grp in ((0, 5, 1, 2, 3, 4), (6, 7, 8, 9, 12)):
         tot = sum(v[k] for k in grp)
         for k in grp:
             if v[k]:
