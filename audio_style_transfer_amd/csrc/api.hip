@@ -642,7 +642,7 @@ int ast_embeds(ast_ctx* x, const float* xd, float* emb_c, float* emb_s, void* st
     }
     if (emb_s && c.gatys) {
         GatysArgs g = gatys_args(x);
-        launch_gatys_fwd(g, x->bf, s);
+        launch_gatys_fwd(g, x->split ? 2 : (x->bf ? 1 : 0), s);
         GatysStyleArgs a = gatys_style_args(x);
         a.embs = emb_s;
         launch_style_gatys(a, s);
@@ -711,7 +711,7 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     tmark(x, s);
     if (c.gatys) {
         GatysArgs g = gatys_args(x);
-        launch_gatys_fwd(g, x->bf, s);
+        launch_gatys_fwd(g, x->split ? 2 : (x->bf ? 1 : 0), s);
         tmark(x, s);
         GatysStyleArgs sa = gatys_style_args(x);
         sa.phi = x->phi_s;
@@ -719,7 +719,7 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
         sa.smat = x->smat; sa.smatb = x->smatb; sa.spart = x->spart;
         launch_style_gatys(sa, s);
         tmark(x, s);
-        launch_gatys_bwd(g, x->bf, s);
+        launch_gatys_bwd(g, x->split ? 2 : (x->bf ? 1 : 0), s);
     } else {
         GramArgs g = gram_args(x);
         launch_gram_fwd_any(x, g, s);

@@ -275,8 +275,8 @@ void launch_gram_fwd_s(const GramArgs& a, hipStream_t s);   // precision 2: bf16
 void launch_gram_bwd_s(const GramArgs& a, hipStream_t s);
 void launch_gram_bwd(const GramArgs& a, hipStream_t s);
 void launch_style_ours(const StyleArgs& a, hipStream_t s);
-void launch_gatys_fwd(const GatysArgs& a, bool bf16, hipStream_t s);
-void launch_gatys_bwd(const GatysArgs& a, bool bf16, hipStream_t s);
+void launch_gatys_fwd(const GatysArgs& a, int precision, hipStream_t s);   // 0 fp32, 1 bf16, 2 split
+void launch_gatys_bwd(const GatysArgs& a, int precision, hipStream_t s);
 void launch_style_gatys(const GatysStyleArgs& a, hipStream_t s);
 constexpr int GY_ROWS = 512;    // Gatys bwd: time rows per workgroup
 void launch_content(const ContentArgs& a, hipStream_t s);

@@ -292,6 +292,180 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_f32(GatysArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// split mode (precision 2): fp32 activations, bf16 MFMA on two-term operands x = xh + xl
+// (xh = bf16(x), xl = bf16(x - xh)), products hi.hi + hi.lo + lo.hi, fp32 accumulation (the
+// ours-Gram's scheme, gram_split.hip).  fwd: fp32 rows -> registers one stage ahead -> split
+// into the two swizzled bf16 images of k_gatys_fwd_bf16 -> the same transposed fragment reads,
+// three MFMAs per tile and k-step.  bwd: S~ split into two LDS images, E rows split per lane.
+
+__device__ __forceinline__ void split2g(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+    hi = pack2(x0, x1);
+    lo = pack2(x0 - bflo(hi), x1 - bfhi(hi));
+}
+
+__global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
+    __shared__ __attribute__((aligned(1024))) u16 Lh[GYB * C];   // [t][c] bf16 hi, swizzled
+    __shared__ __attribute__((aligned(1024))) u16 Ll[GYB * C];   // lo
+    int b, u, ch;
+    gatys_decode(a, b, u, ch);
+    const int tlen = a.T / a.nchunk;
+    const int nt = tlen / GYB;
+    const float* E = (const float*)a.act + (size_t)a.uid[u] * a.tstride +
+                     ((size_t)b * a.T + (size_t)ch * tlen) * C;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // staging: float4 f = tid + 256 k: row (tid >> 5) + 8 k, channels 4 (tid & 31) .. + 3
+    const int c4 = tid & 31, r0 = tid >> 5;
+    float4 v[8];
+    auto load = [&](int k) {
+        const float* src = E + (size_t)k * GYB * C + (size_t)r0 * C + 4 * c4;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(src + (size_t)(8 * q) * C);
+    };
+    // image element offset of (row r, channels 4 c4 ..): 16-B chunk (c4 >> 1) swizzled by
+    // ((r & 3) << 2), half (c4 & 1)
+    auto img = [&](int r) { return r * C + (((c4 >> 1) ^ ((r & 3) << 2)) * 8) + (c4 & 1) * 4; };
+    const int kg = lane >> 5, g16 = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
+    int aoff[2], boff[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int I = 2 * (w >> 1) + t, J = 2 * (w & 1) + t;
+        aoff[t] = (8 * kg + q) * C + (((4 * I + 2 * g16 + (p >> 1)) ^ (q << 2)) * 8) + (p & 1) * 4;
+        boff[t] = (8 * kg + q) * C + (((4 * J + 2 * g16 + (p >> 1)) ^ (q << 2)) * 8) + (p & 1) * 4;
+    }
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+            for (int e = 0; e < 16; ++e) acc[ii][jj][e] = 0.f;
+    auto frag = [&](const u16* L, int off, int s) {
+        const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(L + off + (16 * s) * C));
+        const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(L + off + (16 * s + 4) * C));
+        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    load(0);
+    for (int k = 0; k < nt; ++k) {
+        __syncthreads();   // the previous stage's fragment reads are done
+#pragma unroll
+        for (int qq = 0; qq < 8; ++qq) {
+            const int r = r0 + 8 * qq;
+            uint32_t h0, l0, h1, l1;
+            split2g(v[qq].x, v[qq].y, h0, l0);
+            split2g(v[qq].z, v[qq].w, h1, l1);
+            *reinterpret_cast<uint2*>(&Lh[img(r)]) = make_uint2(h0, h1);
+            *reinterpret_cast<uint2*>(&Ll[img(r)]) = make_uint2(l0, l1);
+        }
+        if (k + 1 < nt) load(k + 1);      // next stage in flight during this one
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < GYB / 16; ++s) {
+            bf16x8 fah[2], fal[2], fbh[2], fbl[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                fah[t] = frag(Lh, aoff[t], s);
+                fal[t] = frag(Ll, aoff[t], s);
+                fbh[t] = frag(Lh, boff[t], s);
+                fbl[t] = frag(Ll, boff[t], s);
+            }
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fah[ii], fbh[jj], acc[ii][jj], 0, 0, 0);
+                    acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fah[ii], fbl[jj], acc[ii][jj], 0, 0, 0);
+                    acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fal[ii], fbh[jj], acc[ii][jj], 0, 0, 0);
+                }
+        }
+    }
+    store_gpart(a, b, u, ch, acc, w, lane);
+}
+
+__global__ void __launch_bounds__(256) k_gatys_bwd_s(GatysArgs a) {
+    __shared__ __attribute__((aligned(16))) u16 Sh[C * SBS];   // S~ hi
+    __shared__ __attribute__((aligned(16))) u16 Sl[C * SBS];   // S~ lo
+    const int tilesPer = a.T / GY_ROWS;
+    int bid = blockIdx.x;
+    const int tile = bid % tilesPer; bid /= tilesPer;
+    const int u = bid % a.nu, b = bid / a.nu;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float* S = a.smat + ((size_t)b * a.nu + u) * (C * C);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int i = tid + 256 * k, row = i >> 4, c8 = i & 15;   // 8 values per piece
+        const float4 x0 = *reinterpret_cast<const float4*>(S + row * C + c8 * 8);
+        const float4 x1 = *reinterpret_cast<const float4*>(S + row * C + c8 * 8 + 4);
+        uint32_t h[4], l[4];
+        split2g(x0.x, x0.y, h[0], l[0]);
+        split2g(x0.z, x0.w, h[1], l[1]);
+        split2g(x1.x, x1.y, h[2], l[2]);
+        split2g(x1.z, x1.w, h[3], l[3]);
+        *reinterpret_cast<uint4*>(&Sh[row * SBS + c8 * 8]) = make_uint4(h[0], h[1], h[2], h[3]);
+        *reinterpret_cast<uint4*>(&Sl[row * SBS + c8 * 8]) = make_uint4(l[0], l[1], l[2], l[3]);
+    }
+    float* E = (float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;
+    const float* CG = (const float*)a.cg[u];
+    if (CG) CG += (size_t)b * a.T * C;
+    const int j = lane & 31, kg = lane >> 5;
+    const int rows_w = GY_ROWS / 4;
+    const int t0 = tile * GY_ROWS + w * rows_w;
+    // lane (j, kg): time row t + j, channels kg 64 .. + 63 as 8 k-steps of 8
+    float4 cur[16], nxt[16];
+    auto loadB = [&](int t, float4 (&bb)[16]) {
+        const float4* src = reinterpret_cast<const float4*>(E + (size_t)(t + j) * C + kg * 64);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) bb[s] = src[s];
+    };
+    loadB(t0, cur);
+    __syncthreads();
+    const u16* Ah = Sh + j * SBS + kg * 64;
+    const u16* Al = Sl + j * SBS + kg * 64;
+    for (int n = 0; n < rows_w / 32; ++n) {
+        const int t = t0 + 32 * n;
+        if (n + 1 < rows_w / 32) loadB(t + 32, nxt);
+        f32x16 acc[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            uint32_t h[4], l[4];
+            split2g(cur[2 * s].x, cur[2 * s].y, h[0], l[0]);
+            split2g(cur[2 * s].z, cur[2 * s].w, h[1], l[1]);
+            split2g(cur[2 * s + 1].x, cur[2 * s + 1].y, h[2], l[2]);
+            split2g(cur[2 * s + 1].z, cur[2 * s + 1].w, h[3], l[3]);
+            const uint4 bh = make_uint4(h[0], h[1], h[2], h[3]), bl = make_uint4(l[0], l[1], l[2], l[3]);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const uint4 ah = *reinterpret_cast<const uint4*>(Ah + 32 * m * SBS + 8 * s);
+                const uint4 al = *reinterpret_cast<const uint4*>(Al + 32 * m * SBS + 8 * s);
+                acc[m] = mfma_bf16(ah, bh, acc[m]);
+                acc[m] = mfma_bf16(ah, bl, acc[m]);
+                acc[m] = mfma_bf16(al, bh, acc[m]);
+            }
+        }
+        // lane holds time t + j, channels 32m + 8g + 4kg + 0..3 in acc[m][4g..4g+3]
+        float* out = E + (size_t)(t + j) * C + 4 * kg;
+        const float* cgr = CG ? CG + (size_t)(t + j) * C + 4 * kg : nullptr;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int c = 32 * m + 8 * g;
+                float4 o = make_float4(acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]);
+                if (cgr) {
+                    const float4 cv = *reinterpret_cast<const float4*>(cgr + c);
+                    o.x += cv.x; o.y += cv.y; o.z += cv.z; o.w += cv.w;
+                }
+                *reinterpret_cast<float4*>(out + c) = o;
+            }
+        if (n + 1 < rows_w / 32) {
+#pragma unroll
+            for (int s = 0; s < 16; ++s) cur[s] = nxt[s];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // style loss: one workgroup per (clip, unique tensor); l2-normalise (methods.py:74), loss vs
 // phi (methods.py:118-119), d/dG through the normalisation, S~ = sum dG + dG^T.
 
@@ -372,14 +546,16 @@ __global__ void __launch_bounds__(256) k_style_gatys(GatysStyleArgs a) {
     }
 }
 
-void launch_gatys_fwd(const GatysArgs& a, bool bf16, hipStream_t s) {
+void launch_gatys_fwd(const GatysArgs& a, int precision, hipStream_t s) {
     const dim3 g(a.B * a.nu * a.nchunk);
-    if (bf16) hipLaunchKernelGGL(k_gatys_fwd_bf16, g, dim3(256), 0, s, a);
+    if (precision == 1) hipLaunchKernelGGL(k_gatys_fwd_bf16, g, dim3(256), 0, s, a);
+    else if (precision == 2) hipLaunchKernelGGL(k_gatys_fwd_s, g, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_gatys_fwd_f32, g, dim3(256), 0, s, a);
 }
-void launch_gatys_bwd(const GatysArgs& a, bool bf16, hipStream_t s) {
+void launch_gatys_bwd(const GatysArgs& a, int precision, hipStream_t s) {
     const dim3 g(a.B * a.nu * (a.T / GY_ROWS));
-    if (bf16) hipLaunchKernelGGL(k_gatys_bwd_bf16, g, dim3(256), 0, s, a);
+    if (precision == 1) hipLaunchKernelGGL(k_gatys_bwd_bf16, g, dim3(256), 0, s, a);
+    else if (precision == 2) hipLaunchKernelGGL(k_gatys_bwd_s, g, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_gatys_bwd_f32, g, dim3(256), 0, s, a);
 }
 void launch_style_gatys(const GatysStyleArgs& a, hipStream_t s) {
