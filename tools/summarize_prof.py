@@ -1,8 +1,9 @@
 """Summarise a tools/profile.sh run into profiles/ (committed evidence).
 
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats, verbatim) and
-profiles/<tag>_summary.json: per kernel, average duration and HBM traffic per launch from
-the separate FETCH_SIZE / WRITE_SIZE passes.  gfx950 correction (MI355X_MICROARCH.md §HBM):
+profiles/<tag>_summary.json: per kernel and grid size (from the kernel trace, so the bench's
+small side-check launches do not dilute the bench-sized ones), average duration and HBM
+traffic per launch from the separate FETCH_SIZE / WRITE_SIZE passes.  gfx950 correction (MI355X_MICROARCH.md §HBM):
 FETCH_SIZE counts half the bytes of a wide (16 B/lane) coalesced read, so fetched bytes =
 2 * FETCH_SIZE * 1024; WRITE_SIZE reads exactly for 16-B stores: written = WRITE_SIZE * 1024.
 Also (re)writes profiles/traffic.json for bench.py's roofline.traffic field.
@@ -22,7 +23,19 @@ def counters(path, name):
     with open(path) as f:
         for row in csv.DictReader(f):
             if row['Counter_Name'] == name:
-                per[row['Kernel_Name']].append(float(row['Counter_Value']))
+                per[(row['Kernel_Name'], int(row['Grid_Size']))].append(float(row['Counter_Value']))
+    return per
+
+
+def launches(path):
+    """Per (kernel, grid size in threads) durations from the kernel trace: the bench's side
+    checks launch the same kernels on small batches, which the --stats averages mix in."""
+    per = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            grid = int(row['Grid_Size_X']) * int(row['Grid_Size_Y']) * int(row['Grid_Size_Z'])
+            per[(row['Kernel_Name'], grid)].append(
+                (int(row['End_Timestamp']) - int(row['Start_Timestamp'])) / 1e6)
     return per
 
 
@@ -33,14 +46,14 @@ def main(tag, precision, clips, T):
     shutil.copy(os.path.join(src, 'trace', 'run_kernel_stats.csv'),
                 os.path.join(dst, tag + '_kernel_stats.csv'))
     stats = {}
-    with open(os.path.join(src, 'trace', 'run_kernel_stats.csv')) as f:
-        for row in csv.DictReader(f):
-            stats[row['Name']] = {'calls': int(row['Calls']), 'avg_ms': float(row['AverageNs']) / 1e6,
-                                  'total_ms': float(row['TotalDurationNs']) / 1e6,
-                                  'pct': float(row['Percentage'])}
+    for (name, grid), ds in launches(os.path.join(src, 'trace', 'run_kernel_trace.csv')).items():
+        stats['%s@%d' % (name, grid)] = {'name': name, 'grid_threads': grid, 'calls': len(ds),
+                                         'avg_ms': sum(ds) / len(ds), 'total_ms': sum(ds),
+                                         'min_ms': min(ds), 'max_ms': max(ds)}
     fetch = counters(os.path.join(src, 'fetch', 'run_counter_collection.csv'), 'FETCH_SIZE')
     write = counters(os.path.join(src, 'write', 'run_counter_collection.csv'), 'WRITE_SIZE')
-    for k, v in stats.items():
+    for v in stats.values():
+        k = (v['name'], v['grid_threads'])
         if k in fetch:
             v['fetch_bytes_raw'] = sum(fetch[k]) / len(fetch[k]) * 1024
             v['fetch_bytes_corrected'] = 2 * v['fetch_bytes_raw']
@@ -52,8 +65,10 @@ def main(tag, precision, clips, T):
     summary = {'tag': tag, 'precision': precision, 'clips': clips, 'T': T, 'kernels': stats}
     with open(os.path.join(dst, tag + '_summary.json'), 'w') as f:
         json.dump(summary, f, indent=1)
-    def pick(name):   # every layout / template variant of the kernel, weighted by calls
+    def pick(name):   # the bench-sized launches (largest grid) of every template variant
         ks = [k for k in stats if name in k and 'hbm_bytes_per_launch' in stats[k]]
+        big = max((stats[k]['grid_threads'] for k in ks), default=0)
+        ks = [k for k in ks if stats[k]['grid_threads'] == big]
         n = sum(stats[k]['calls'] for k in ks)
         if not n:
             return {}
@@ -69,8 +84,8 @@ def main(tag, precision, clips, T):
         with open(os.path.join(dst, 'traffic.json'), 'w') as f:
             json.dump(tj, f, indent=1)
     for k, v in sorted(stats.items(), key=lambda kv: -kv[1]['total_ms'])[:10]:
-        print('%-60s calls %4d avg %8.3f ms  hbm/launch %s' % (
-            k[:60], v['calls'], v['avg_ms'],
+        print('%-40s calls %4d avg %8.3f ms  hbm/launch %s' % (
+            k[:40], v['calls'], v['avg_ms'],
             '%.3f GB (%.0f GB/s)' % (v['hbm_bytes_per_launch'] / 1e9, v['hbm_GBs'])
             if 'hbm_bytes_per_launch' in v else '-'))
 
