@@ -218,7 +218,7 @@ def grad_check(Eng, precision, dev):
             'loss_rel': abs(loss - float(g['ours_parts'][0])) / abs(float(g['ours_parts'][0]))}
 
 
-def cpu_baseline(T, budget_s):
+def cpu_baseline(T, budget_s, gatys=False):
     """Time the torch-CPU fp32 restatement of the reference path (oracle/torch_restatement.py:
     F.conv1d forward, autograd backward; the reference's TF-CPU path needs TensorFlow, absent
     here) on this host's cores, on a bounded sample of the same workload: whole loss+grad
@@ -231,10 +231,10 @@ def cpu_baseline(T, budget_s):
     cores = min(cores, os.cpu_count())
     torch.set_num_threads(cores)
     W = synthetic_weights(0)
-    kw = dict(cont_ids=[29], style_ids=list(range(30)))
+    kw = dict(cont_ids=[29], style_ids=list(range(30)), gatys=gatys)
     xc = mu_law_numpy(synthetic_clips(1, T, 1000)[0]).astype(np.float64)
     phi_c = np.zeros((T, 128), np.float32)
-    phi_s = np.zeros((128, 30, 30), np.float32)
+    phi_s = np.zeros((30, 128, 128) if gatys else (128, 30, 30), np.float32)
     x = xc + np.random.default_rng(0).normal(0, 4, T)
     TR.cpu_step(x, W, phi_c=phi_c, phi_s=phi_s, **kw)      # warm-up (allocator, threads)
     n = 0
@@ -250,8 +250,9 @@ def cpu_baseline(T, budget_s):
             'cores': int(cores), 'host_cpus': os.cpu_count(), 'kind': 'port',
             'sample': '%d loss+grad evaluations of one %d-sample clip in %.1f s = %.3f clip-evals/s '
                       '(torch-CPU fp32 restatement: conv1d forward + autograd backward, 30 blocks, '
-                      'ours-Gram L=30, STFT regulariser evaluated as TF does); scaled to the '
-                      '256-clip batch' % (n, T, el, clip_evals_per_s),
+                      '%s L=30, STFT regulariser evaluated as TF does); scaled to the '
+                      '256-clip batch' % (n, T, el, clip_evals_per_s,
+                                          'Gatys Gram' if gatys else 'ours-Gram'),
             'clip_evals_per_s': clip_evals_per_s,
             'note': 'a reported baseline, not the target'}
 
@@ -373,7 +374,7 @@ def rank_main(args):
         out.update(grad_check(Eng, args.precision, dev))
     out.update(side)
     if ws == 1 and args.cpu_baseline_seconds > 0:
-        out['cpu_baseline'] = cpu_baseline(T, args.cpu_baseline_seconds)
+        out['cpu_baseline'] = cpu_baseline(T, args.cpu_baseline_seconds, args.gatys)
     print(json.dumps(out), flush=True)
     barrier(ws)
     return out

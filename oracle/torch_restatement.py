@@ -72,14 +72,15 @@ def loss_fn(x, W, *, cont_ids, style_ids, phi_c, phi_s, lambd=100.0, gamma=0.0, 
     return total, content, style, reg
 
 
-def cpu_step(x, W, *, cont_ids, style_ids, phi_c, phi_s, lambd=100.0, dtype=torch.float32):
+def cpu_step(x, W, *, cont_ids, style_ids, phi_c, phi_s, lambd=100.0, gatys=False,
+             dtype=torch.float32):
     """One loss+grad evaluation of one clip (the reference's CPU path restated: fp32 conv1d
     forward, autograd backward to x).  Returns (total, grad [T])."""
     xt = torch.as_tensor(x, dtype=dtype).detach().clone().requires_grad_(True)
     total, _, _, _ = loss_fn(xt, W, cont_ids=cont_ids, style_ids=style_ids, phi_c=phi_c,
-                             phi_s=phi_s, lambd=lambd, dtype=dtype)
+                             phi_s=phi_s, lambd=lambd, gatys=gatys, dtype=dtype)
     g, = torch.autograd.grad(total, xt)
-    return float(total), g
+    return float(total.detach()), g
 
 
 def stft_reg(x):
