@@ -18,7 +18,7 @@ EXPORTS = ('ast_create', 'ast_destroy', 'ast_workspace_bytes', 'ast_set_weight',
            'ast_get_extract', 'ast_embeds', 'ast_content_cols', 'ast_set_targets',
            'ast_set_gamma', 'ast_loss_grad', 'ast_adam_step', 'ast_adam_step_dev',
            'ast_lbfgs_workspace_bytes', 'ast_lbfgs_begin', 'ast_lbfgs_step', 'ast_lbfgs_state',
-           'ast_timing', 'ast_timing_read',
+           'ast_timing', 'ast_timing_read', 'ast_ot_admm',
            'ast_last_error')
 
 
@@ -70,6 +70,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         'ast_lbfgs_state': (i, [vp, vp, vp, vp, vp]),
         'ast_timing': (i, [vp, i]),
         'ast_timing_read': (i, [vp, fp, i]),
+        'ast_ot_admm': (i, [vp, vp, i, i, i, i, ctypes.c_double, ctypes.c_double, vp, vp, vp, vp]),
         'ast_last_error': (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():

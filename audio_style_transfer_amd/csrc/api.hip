@@ -368,6 +368,21 @@ extern "C" {
 
 const char* ast_last_error(void) { return g_err.c_str(); }
 
+int ast_ot_admm(const double* p_mod, const double* p_ref, int nprob, int n1, int n2, int d,
+                double eps, double miter, double* plan, double* pal, int* iters, void* stream) {
+    if (nprob < 0 || n1 < 1 || n2 < 1 || d < 1)
+        return fail(AST_E_ARG, "ast_ot_admm: need nprob >= 0 and n1, n2, d >= 1");
+    if ((long long)n1 * n2 > ot_max_cells())
+        return fail(AST_E_ARG, "ast_ot_admm: n1 * n2 must be <= " + std::to_string(ot_max_cells()));
+    if (!(eps > 0.0) || !(miter >= 0.0))
+        return fail(AST_E_ARG, "ast_ot_admm: eps must be > 0 and miter >= 0");
+    if (nprob == 0) return 0;
+    if (!p_mod || !p_ref || !plan) return fail(AST_E_ARG, "ast_ot_admm: null buffer");
+    launch_ot_admm(p_mod, p_ref, nprob, n1, n2, d, eps, miter, plan, pal, iters, S(stream));
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 // Diagnostic hook (not in astyle.h): device buffer of 12 u64 phase-cycle sums that
 // -DASTYLE_STAMPS builds of the bf16 block kernels accumulate into; NULL disables.
 int ast_debug_stamps(void* dev_u64x16) {

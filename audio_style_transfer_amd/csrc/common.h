@@ -315,4 +315,10 @@ void launch_adam(float* x, float* m, float* v, const float* g, size_t n, float l
 void launch_adam_dev(float* x, float* m, float* v, const float* g, size_t n, int* step_dev,
                      float lr, float b1, float b2, float eps, hipStream_t s);
 
+// batched ADMM optimal transport between palettes (ot_admm.hip, optimal_transport.py:77-162)
+size_t ot_lds_bytes(int n1, int n2);
+int ot_max_cells();
+void launch_ot_admm(const double* p_mod, const double* p_ref, int nprob, int n1, int n2, int d,
+                    double eps, double miter, double* plan, double* pal, int* iters, hipStream_t s);
+
 }  // namespace ast

@@ -4,8 +4,11 @@ Same argparse surface (methods.py:243-269), same output layout (utils.gt_s_path 
 ori.wav, style.wav, ep-N.wav, gram/spectrogram PNGs), same optimisation protocol: per epoch one
 scipy L-BFGS-B minimize(maxiter=100) whose every function evaluation is one ast_loss_grad
 (ScipyOptimizerInterface, methods.py:132-137,167), early stop when an epoch used < 50
-evaluations (methods.py:180).  Additions: --optimizer device (the same L-BFGS-B on the GPU),
---precision bf16, --weights (npz of TF-named encoder variables).
+evaluations (methods.py:180), the four loss scalars of every evaluation written to a TF event
+file in the log dir (methods.py:127-130,156; summary.EventWriter).  Additions: --optimizer
+device (the same L-BFGS-B on the GPU), --precision split|bf16, --weights (npz of TF-named
+encoder variables), --resume (continue after the last finished epoch: each epoch's end point
+is saved as <savepath>/state.npz; an epoch is a fresh minimize call, so x is the whole state).
 
 The TF checkpoint itself cannot be read here (no TF): --ckpt_path is
 honoured when it points at an .npz of TF-named arrays; otherwise seeded synthetic weights
@@ -22,7 +25,7 @@ import warnings
 import numpy as np
 import torch
 
-from . import utils
+from . import summary, utils
 from .engine import StyleEngine, resolve_style_ids
 from .weights import synthetic_weights
 
@@ -113,12 +116,19 @@ class GatysNet(object):
             utils.show_gram(phi, figdir=self.figdir, gatys=self.gatys)
         return phi
 
-    def l_bfgs(self, *args, x0=None, log=print, optimizer='scipy', maxiter=100, **kw):
+    def l_bfgs(self, *args, x0=None, log=print, optimizer='scipy', maxiter=100, resume=False,
+               **kw):
         """methods.py:140-181 with scipy L-BFGS-B driving ast_loss_grad (``optimizer='scipy'``,
         one host round trip per evaluation, as the reference), or the same L-BFGS-B run on the
         device (``'device'``: ast_lbfgs_*, no round trip; progress is logged per epoch).
         Accepts the reference's l_bfgs(sess, phi_c, phi_s, epochs, lambd, gamma) as well.  Every
-        epoch starts from the float32 rounding of its point, as the TF variable does."""
+        epoch starts from the float32 rounding of its point, as the TF variable does.
+
+        Each evaluation's (content, style, regularizer, main) losses go to the log dir's event
+        file at step i_ + i (methods.py:147-157: i counts this epoch's evaluations, i_ is the
+        previous epoch's count).  After every epoch its end point, index and count are saved
+        to <savepath>/state.npz; ``resume=True`` continues from there (an epoch is a fresh
+        minimize call, methods.py:167, so nothing else carries over)."""
         from scipy.optimize import minimize
         names = ('phi_c', 'phi_s', 'epochs', 'lambd', 'gamma')
         vals = dict(zip(names, _drop_sess(args)))
@@ -135,6 +145,21 @@ class GatysNet(object):
         xd = torch.empty(1, T, device=self.device)
         state = {'i': 0, 'i_': 0, 'since': time.time()}
         history = []
+        start_ep = 0
+        ckpt = os.path.join(self.savepath, 'state.npz')
+        if resume and os.path.isfile(ckpt):
+            with np.load(ckpt, allow_pickle=False) as z:
+                x = np.asarray(z['x'], dtype=np.float64)
+                start_ep, state['i_'] = int(z['ep']) + 1, int(z['i_'])
+            log('resuming after epoch %d (%d evaluations) from %s' % (start_ep, state['i_'], ckpt))
+            if state['i_'] < 50:                                          # it had stopped
+                self.history = history
+                return x
+        writer = summary.EventWriter(self.logdir)
+
+        def scalars(p, step):
+            writer.add_scalars({'loss/content_loss': p[1], 'loss/style_loss': p[2],
+                                'loss/regularizer': p[3], 'loss/main_loss': p[0]}, step)
 
         def fg(v):
             xd.copy_(torch.from_numpy(v.astype(np.float32)).view(1, T))
@@ -142,6 +167,7 @@ class GatysNet(object):
             p = parts[0].cpu().numpy().astype(np.float64)
             loss, reg = float(p[0]), float(p[3])
             history.append((loss, float(p[1]), float(p[2]), reg))
+            scalars(p, state['i_'] + state['i'])
             if not state['i'] % 5:                                       # methods.py:152-155
                 log('Ep {0:}/{1:}-it {2:}({3:})-tlapse {4:.4f}s-loss{5:.4f}-{6:.4f}-{7:.4f}-{8:.4f}'.format(
                     state['ep'] + 1, epochs, state['i'], state['i_'], time.time() - state['since'],
@@ -153,20 +179,24 @@ class GatysNet(object):
         if optimizer == 'device':
             from .engine import LbfgsLoop
             loop = LbfgsLoop(eng, maxiter=maxiter)
-        for ep in range(epochs):
+        for ep in range(start_ep, epochs):
             state['ep'], state['i'] = ep, 0
             if loop is None:
                 res = minimize(fg, x, jac=True, method='L-BFGS-B', options={'maxiter': maxiter})
                 x = res.x.astype(np.float32).astype(np.float64)   # next epoch: fp32(res.x)
             else:
-                info = loop.minimize(torch.tensor(x[None], dtype=torch.float64) if ep == 0 else None)
+                info = loop.minimize(torch.tensor(x[None], dtype=torch.float64)
+                                     if ep == start_ep else None)
                 x = loop.state(with_x=True)[1][0].cpu().numpy()
                 state['i'] = int(info[0, 2])
                 p = loop.parts[0].cpu().numpy().astype(np.float64)
                 history.append((float(p[0]), float(p[1]), float(p[2]), float(p[3])))
+                scalars(p, state['i_'] + state['i'] - 1)      # the epoch's last evaluation
                 log('Ep {0:}/{1:}-it {2:}-tlapse {3:.4f}s-loss{4:.4f}-{5:.4f}-{6:.4f}-{7:.4f}'.format(
                     ep + 1, epochs, state['i'], time.time() - state['since'], *p))
             state['i_'] = state['i']
+            writer.flush()
+            np.savez(ckpt, x=x.astype(np.float32).astype(np.float64), ep=ep, i_=state['i_'])
             audio = utils.inv_mu_law_numpy(x[None])[0, self.late:-self.late]
             sp = os.path.join(self.savepath, 'ep-{}.wav'.format(ep))
             utils.write_wav(sp, audio / np.max(audio), sr=self.sr)        # methods.py:176
@@ -176,11 +206,12 @@ class GatysNet(object):
                 utils.show_gram(grams[0].cpu().numpy(), ep + 1, self.figdir, gatys=self.gatys)
             if state['i_'] < 50:                                          # methods.py:180-181
                 break
+        writer.close()
         self.history = history
         return x
 
     def run(self, cont_file, source, target, epochs, lambd=0.1, gamma=0.1, audio_channel=0,
-            start=1.0):
+            start=1.0, resume=False):
         """methods.py:183-216."""
         phi_t = self.get_style_phi(target)
         phi_s = self.get_style_phi(source, show_mat=False)
@@ -196,7 +227,7 @@ class GatysNet(object):
         phi = phi + phi_t - phi_s
         phi = phi / np.sqrt(np.maximum(np.sum(phi * phi, axis=(1, 2), keepdims=True), 1e-12))
         x = self.l_bfgs(phi_c, phi, epochs=epochs, lambd=lambd, gamma=gamma,
-                        optimizer=self.optimizer)
+                        optimizer=self.optimizer, resume=resume)
         return utils.inv_mu_law_numpy(x[None])[0]
 
 
@@ -210,7 +241,7 @@ def get_fpath(fn, args):
     return os.path.join(args.dir, fn) + '.wav'
 
 
-EXTRA_FLAGS = ('precision', 'weights', 'no_plots', 'optimizer')
+EXTRA_FLAGS = ('precision', 'weights', 'no_plots', 'optimizer', 'resume')
 
 
 def piece_work(args):
@@ -225,11 +256,11 @@ def piece_work(args):
                     precision=args.precision, weights=weights, plots=not args.no_plots,
                     optimizer=args.optimizer)
     return test.run(content, content, style, epochs=args.epochs, lambd=args.lambd,
-                    gamma=args.gamma, start=args.start)
+                    gamma=args.gamma, start=args.start, resume=args.resume)
 
 
 def make_parser():
-    """methods.py:244-267, plus --precision / --weights / --no_plots."""
+    """methods.py:244-267, plus --precision / --weights / --no_plots / --optimizer / --resume."""
     parser = argparse.ArgumentParser()
     parser.add_argument('cont_fn', help='relative content file name')
     parser.add_argument('style_fn', help='relative style file name')
@@ -252,13 +283,16 @@ def make_parser():
     parser.add_argument('--outdir', help='path to output', nargs='?', default='./data/out')
     parser.add_argument('--logdir', help='path to logs', nargs='?', default='./log')
     parser.add_argument('--cmt')
-    parser.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'],
-                        help='fp32: reference numerics; bf16: bf16 storage + bf16 MFMA')
+    parser.add_argument('--precision', default='fp32', choices=['fp32', 'split', 'bf16'],
+                        help='fp32: reference numerics; split: fp32 storage, split-fp16/bf16 '
+                             'MFMA (fp32-accurate, faster); bf16: bf16 storage + bf16 MFMA')
     parser.add_argument('--weights', default=None, help='npz of TF-named encoder weights')
     parser.add_argument('--no_plots', action='store_true', help='skip the Gram PNGs')
     parser.add_argument('--optimizer', default='scipy', choices=['scipy', 'device'],
                         help='scipy: host L-BFGS-B per evaluation (reference); device: the same '
                              'L-BFGS-B on the GPU (ast_lbfgs_*)')
+    parser.add_argument('--resume', action='store_true',
+                        help='continue after the last finished epoch saved in the output dir')
     return parser
 
 

@@ -137,6 +137,16 @@ int ast_lbfgs_state(ast_ctx* ctx, const void* ws_dev, int* info_dev, double* x64
 int ast_timing(ast_ctx* ctx, int enable);
 int ast_timing_read(ast_ctx* ctx, float* out, int n);
 
+/* Batched ADMM optimal transport between NMF palettes: OT_ADMM + transform_palette
+ * (optimal_transport.py:77-162; compute_permutation = both).  For each of nprob problems,
+ * p_mod_dev [n1, d] and p_ref_dev [n2, d] float64 -> plan_dev [n1, n2] (the transport plan),
+ * palette_dev [n1, d] (p_ref moved onto p_mod's palette: plan p_ref / (row sums + 1e-10);
+ * NULL = skip), iters_dev [nprob] int (ADMM iterations; NULL = skip).  eps, miter as OT_ADMM's
+ * (1e-4, 1e5).  Needs n1 n2 <= 4096.  fp64, one workgroup per problem; no context. */
+int ast_ot_admm(const double* p_mod_dev, const double* p_ref_dev, int nprob, int n1, int n2, int d,
+                double eps, double miter, double* plan_dev, double* palette_dev, int* iters_dev,
+                void* stream);
+
 const char* ast_last_error(void);
 
 #ifdef __cplusplus

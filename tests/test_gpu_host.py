@@ -137,3 +137,50 @@ def test_gatysnet_device_optimizer_matches_scipy_path(tmp_path, weights):
     assert os.path.isfile(out / 'ep-0.wav') and not os.path.isfile(out / 'ep-1.wav')
     assert rel(xb, xa) <= 1e-6, rel(xb, xa)
     assert np.array_equal(xa, xa.astype(np.float32).astype(np.float64))   # fp32-rounded epochs
+
+
+def test_event_log_and_resume(tmp_path, weights):
+    """methods.py:127-130,147-157: every evaluation's four loss scalars in a TF event file at
+    step i_ + i; and --resume: an epoch continued from <savepath>/state.npz lands on the same
+    point as the same epoch run directly from that point (an epoch is a fresh minimize call)."""
+    import glob
+    from audio_style_transfer_amd import summary
+    from audio_style_transfer_amd.methods import GatysNet
+    T = 4096
+    out = tmp_path / 'out'
+    out.mkdir()
+    net = GatysNet(str(out), None, str(tmp_path / 'log'), str(tmp_path / 'fig'), stack=0,
+                   batch_size=T, cont_lyr_ids=[9], weights=weights, plots=False)
+    xc = O.mu_law_numpy(synthetic_clips(1, T, 1000)[0])
+    xs = O.mu_law_numpy(synthetic_clips(1, T, 5000)[0])
+    kw = dict(cont_ids=[9], style_ids=list(range(10)), gatys=False, nb_channels=128,
+              cnt_channels=128)
+    phi_c, phi_s = O.targets_from_audio(weights, xc, [xs], [xc], **kw)
+    x1 = net.l_bfgs(phi_c, phi_s, epochs=1, lambd=100.0, gamma=0.0, maxiter=4, log=lambda s: None)
+    h = np.array(net.history)
+    files = glob.glob(str(tmp_path / 'log' / 'events.out.tfevents.*'))
+    assert len(files) == 1
+    ev = summary.read_events(files[0])
+    assert ev[0]['file_version'] == 'brain.Event:2'
+    sc = [e for e in ev[1:] if e['scalars']]
+    assert [e['step'] for e in sc] == list(range(len(h)))
+    got = np.array([[e['scalars']['loss/main_loss'], e['scalars']['loss/content_loss'],
+                     e['scalars']['loss/style_loss'], e['scalars']['loss/regularizer']] for e in sc])
+    assert np.array_equal(got, h.astype(np.float32))
+    st = np.load(str(out / 'state.npz'))
+    assert int(st['ep']) == 0 and int(st['i_']) == len(h) and np.array_equal(st['x'], x1)
+    # pretend epoch 0 used 60 evaluations (no early stop), then resume into epoch 1
+    np.savez(str(out / 'state.npz'), x=x1, ep=0, i_=60)
+    x2 = net.l_bfgs(phi_c, phi_s, epochs=2, lambd=100.0, gamma=0.0, maxiter=4, resume=True,
+                    log=lambda s: None)
+    assert os.path.isfile(out / 'ep-1.wav')
+    n2 = len(net.history)
+    files = sorted(glob.glob(str(tmp_path / 'log' / 'events.out.tfevents.*')), key=os.path.getmtime)
+    steps = [e['step'] for e in summary.read_events(files[-1]) if e['scalars']]
+    assert steps == list(range(60, 60 + n2))
+    x3 = net.l_bfgs(phi_c, phi_s, epochs=1, lambd=100.0, gamma=0.0, maxiter=4, x0=x1,
+                    log=lambda s: None)
+    assert np.array_equal(x2, x3)
+    # a finished run (last epoch stopped early) resumes to its saved point without evaluating
+    x4 = net.l_bfgs(phi_c, phi_s, epochs=5, lambd=100.0, gamma=0.0, resume=True, log=lambda s: None)
+    assert np.array_equal(x4, x3) and net.history == []

@@ -1,0 +1,50 @@
+"""The OT palette solver's oracle (oracle/ot_oracle.py, optimal_transport.py:22-162) on the CPU:
+parity unpinned, so it is held to properties the reference's algorithm implies:
+the cost matrix is the Euclidean distance matrix, the plan is non-negative and meets the three
+constraints to the ADMM tolerance, and transform_palette is a row-normalised mix of p_ref."""
+import numpy as np
+import pytest
+from scipy.spatial.distance import cdist
+
+from oracle import ot_oracle as O
+
+CASES = [(5, 10, 128, 0), (10, 5, 128, 1), (3, 7, 4, 2), (12, 9, 16, 3), (1, 4, 8, 4)]
+
+
+def _pal(n1, n2, d, seed):
+    r = np.random.RandomState(seed)
+    return r.rand(n1, d), r.rand(n2, d)
+
+
+@pytest.mark.parametrize('n1,n2,d,seed', CASES)
+def test_oracle_plan_properties(n1, n2, d, seed):
+    w1, w2 = _pal(n1, n2, d, seed)
+    C = O.cost_matrix(w1, w2)
+    assert np.allclose(C, cdist(w1, w2), rtol=1e-13, atol=0)
+    plan, it = O.ot_admm(w1, w2)
+    assert 0 < it < 1e5
+    assert plan.min() >= 0
+    tol = 5e-3
+    assert abs(plan.sum() - 1) <= tol
+    assert np.all(plan.sum(1) <= 1.0 / n1 * (1 + tol))
+    assert np.all(plan.sum(0) <= 1.0 / n2 * (1 + tol))
+    # transport prefers cheap pairs: cost below that of the independent (uniform) coupling
+    Cn = C / C.max()
+    assert (Cn * plan).sum() <= Cn.mean() * (1 + tol)
+    pal = O.transform_palette(w1, w2, plan)
+    assert pal.shape == (n1, d)
+    assert np.all(pal >= w2.min(0) - 1e-9) and np.all(pal <= w2.max(0) + 1e-9)
+    assert np.array_equal(O.compute_permutation(w1, w2), pal)
+
+
+def test_oracle_projections():
+    r = np.random.RandomState(100)
+    x = r.normal(0, 0.05, (6, 9))
+    p = O.project_total(x, 1.0)
+    assert abs(p.sum() - 1.0) < 1e-12 and np.allclose(p - x, (p - x)[0, 0])
+    lo, hi = np.zeros(6), np.full(6, 1 / 6.)
+    q = O.project_row_sums(x, lo, hi)
+    s = q.sum(1)
+    assert np.all(s >= -1e-15) and np.all(s <= 1 / 6. + 1e-15)
+    inside = (x.sum(1) >= 0) & (x.sum(1) <= 1 / 6.)
+    assert np.array_equal(q[inside], x[inside])
