@@ -12,8 +12,10 @@ CSRC = os.path.join(PKG, 'csrc')
 LIB = os.path.join(PKG, 'libastyle.so')
 SOURCES = ['encoder.hip', 'block_fwd_bf16.hip', 'block_bwd_bf16.hip', 'block_fwd_split.hip',
            'block_bwd_split.hip', 'gram.hip', 'gram_bf16.hip', 'gram_split.hip', 'gram_gatys.hip', 'stft_reg.hip',
-           'lbfgs.hip', 'ot_admm.hip', 'api.hip']
+           'lbfgs.hip', 'ot_admm.hip', 'api.hip', 'ckpt.cpp']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+CXX = os.environ.get('CXX', 'g++')          # host-only sources (.cpp)
+CXXFLAGS = ['-O2', '-fPIC', '-std=c++17', '-Wall']
 FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall',
          '-Wno-unused-function', '-munsafe-fp-atomics']
 # per-source extras: the column-owning block kernels keep their weights in AGPRs and need the
@@ -46,13 +48,16 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, exp:
     os.makedirs(objdir, exist_ok=True)
 
     def cc(src):
-        obj = os.path.join(objdir, src.replace('.hip', '.o'))
-        cmd = [HIPCC, *flags, *EXTRA.get(src, []), '-c', os.path.join(CSRC, src), '-o', obj]
+        obj = os.path.join(objdir, src.rsplit('.', 1)[0] + '.o')
+        if src.endswith('.cpp'):
+            cmd = [CXX, *CXXFLAGS, '-c', os.path.join(CSRC, src), '-o', obj]
+        else:
+            cmd = [HIPCC, *flags, *EXTRA.get(src, []), '-c', os.path.join(CSRC, src), '-o', obj]
         if verbose:
             print(' '.join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
-            raise RuntimeError('hipcc failed for %s:\n%s' % (src, r.stderr))
+            raise RuntimeError('%s failed for %s:\n%s' % (cmd[0], src, r.stderr))
         if r.stderr and verbose:
             print(r.stderr, file=sys.stderr)
         return obj

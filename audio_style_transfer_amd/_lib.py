@@ -18,7 +18,8 @@ EXPORTS = ('ast_create', 'ast_destroy', 'ast_workspace_bytes', 'ast_set_weight',
            'ast_get_extract', 'ast_embeds', 'ast_content_cols', 'ast_set_targets',
            'ast_set_gamma', 'ast_loss_grad', 'ast_adam_step', 'ast_adam_step_dev',
            'ast_lbfgs_workspace_bytes', 'ast_lbfgs_begin', 'ast_lbfgs_step', 'ast_lbfgs_state',
-           'ast_timing', 'ast_timing_read', 'ast_ot_admm',
+           'ast_timing', 'ast_timing_read', 'ast_ot_admm', 'ast_ckpt_open', 'ast_ckpt_close',
+           'ast_ckpt_num_entries', 'ast_ckpt_entry', 'ast_ckpt_read_f32', 'ast_restore',
            'ast_last_error')
 
 
@@ -71,6 +72,13 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         'ast_timing': (i, [vp, i]),
         'ast_timing_read': (i, [vp, fp, i]),
         'ast_ot_admm': (i, [vp, vp, i, i, i, i, ctypes.c_double, ctypes.c_double, vp, vp, vp, vp]),
+        'ast_ckpt_open': (i, [ctypes.c_char_p, ctypes.POINTER(vp)]),
+        'ast_ckpt_close': (None, [vp]),
+        'ast_ckpt_num_entries': (i, [vp]),
+        'ast_ckpt_entry': (i, [vp, i, ctypes.c_char_p, sz, ctypes.POINTER(i), ctypes.POINTER(i),
+                               ctypes.POINTER(ctypes.c_int64), i]),
+        'ast_ckpt_read_f32': (i, [vp, ctypes.c_char_p, fp, sz]),
+        'ast_restore': (i, [vp, ctypes.c_char_p]),
         'ast_last_error': (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():

@@ -13,6 +13,7 @@
 
 #include "../../include/astyle.h"
 #include "common.h"
+#include "ckpt.h"
 
 using namespace ast;
 
@@ -86,6 +87,10 @@ uint16_t host_bf16(float f) {   // round to nearest even
 struct Occ { int ext, tensor, off, ncol; };
 
 }  // namespace
+
+namespace ast {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }   // ckpt.cpp
+}  // namespace ast
 
 struct ast_ctx {
     ast_cfg cfg;
@@ -367,6 +372,33 @@ GatysStyleArgs gatys_style_args(ast_ctx* x) {
 extern "C" {
 
 const char* ast_last_error(void) { return g_err.c_str(); }
+
+int ast_restore(ast_ctx* x, const char* prefix) {
+    if (!x || !prefix) return fail(AST_E_ARG, "ast_restore: null argument");
+    Checkpoint ck;
+    std::string err;
+    if (ck.open(prefix, &err)) return fail(AST_E_NAME, err);
+    std::vector<std::string> names = {"ae_startconv/W", "ae_startconv/biases", "ae_bottleneck/W",
+                                      "ae_bottleneck/biases"};
+    for (int l = 1; l <= 30; ++l)
+        for (const char* k : {"ae_dilatedconv_%d/W", "ae_dilatedconv_%d/biases", "ae_res_%d/W",
+                              "ae_res_%d/biases"}) {
+            char b[64];
+            snprintf(b, sizeof b, k, l);
+            names.push_back(b);
+        }
+    std::vector<float> buf;
+    for (const std::string& nm : names) {
+        const CkptEntry* e = ck.find(nm);
+        if (!e) return fail(AST_E_NAME, std::string(prefix) + ": no variable " + nm +
+                                            " (Saver.restore needs every encoder variable)");
+        buf.resize((size_t)e->elements());
+        if (ck.read_f32(*e, buf.data(), &err)) return fail(AST_E_ARG, err);
+        const int rc = ast_set_weight(x, nm.c_str(), buf.data(), buf.size());
+        if (rc) return rc;
+    }
+    return 0;
+}
 
 int ast_ot_admm(const double* p_mod, const double* p_ref, int nprob, int n1, int n2, int d,
                 double eps, double miter, double* plan, double* pal, int* iters, void* stream) {

@@ -114,6 +114,11 @@ class StyleEngine:
                 continue
             _lib.check(rc)
 
+    def restore(self, prefix: str) -> None:
+        """Saver.restore(sess, prefix) (methods.py:79-84): every encoder variable from a TF
+        checkpoint-V2 bundle, read natively by ast_restore."""
+        _lib.check(self.lib.ast_restore(self.h, str(prefix).encode()))
+
     @property
     def style_shape(self):
         L = len(self.style_ids)

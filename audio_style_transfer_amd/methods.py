@@ -10,9 +10,10 @@ device (the same L-BFGS-B on the GPU), --precision split|bf16, --weights (npz of
 encoder variables), --resume (continue after the last finished epoch: each epoch's end point
 is saved as <savepath>/state.npz; an epoch is a fresh minimize call, so x is the whole state).
 
-The TF checkpoint itself cannot be read here (no TF): --ckpt_path is
-honoured when it points at an .npz of TF-named arrays; otherwise seeded synthetic weights
-are used and a warning is printed.
+--ckpt_path is a TF checkpoint-V2 prefix (model.ckpt-200000: .index + .data shards), read by
+libastyle's native reader without TensorFlow, or an .npz of TF-named arrays; when neither
+exists (the NSynth checkpoint is not in this image) seeded synthetic weights are used and a
+warning is printed.
 """
 from __future__ import annotations
 
@@ -25,13 +26,17 @@ import warnings
 import numpy as np
 import torch
 
-from . import summary, utils
+from . import checkpoint, summary, utils
 from .engine import StyleEngine, resolve_style_ids
 from .weights import synthetic_weights
 
 
 def load_weights(path):
-    """TF-named encoder weights from an .npz (allow_pickle=False); None if unavailable."""
+    """TF-named encoder weights (Saver.restore, methods.py:79-84) from a TF checkpoint-V2
+    prefix (<path>.index + data shards, read natively: checkpoint.py) or an .npz
+    (allow_pickle=False); None if neither exists."""
+    if checkpoint.is_checkpoint(path):
+        return checkpoint.encoder_weights(path)
     if path and os.path.isfile(path) and path.endswith('.npz'):
         with np.load(path, allow_pickle=False) as z:
             return {k: z[k] for k in z.files}
@@ -72,7 +77,7 @@ class GatysNet(object):
         if weights is None:
             weights = load_weights(checkpoint_path)
             if weights is None:
-                warnings.warn('checkpoint %r not readable here (TF checkpoint reader not built); '
+                warnings.warn('no checkpoint at %r (neither <prefix>.index nor an .npz); '
                               'using seeded synthetic encoder weights' % checkpoint_path)
                 weights = synthetic_weights(0)
         self.weights = weights

@@ -71,7 +71,7 @@ class ShowNet(object):
         if weights is None:
             weights = load_weights(ckpt_path)
             if weights is None:
-                warnings.warn('checkpoint %r not readable here (TF checkpoint reader not built); '
+                warnings.warn('no checkpoint at %r (neither <prefix>.index nor an .npz); '
                               'using seeded synthetic encoder weights' % ckpt_path)
                 weights = synthetic_weights(0)
         self.engine = build_graph(length, stack, channels, weights=weights, precision=precision,

@@ -34,6 +34,7 @@
 #define ASTYLE_H
 
 #include <stddef.h>
+#include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -136,6 +137,22 @@ int ast_lbfgs_state(ast_ctx* ctx, const void* ws_dev, int* info_dev, double* x64
  * calls timed, out[6] = launches per family per call (blocks). */
 int ast_timing(ast_ctx* ctx, int enable);
 int ast_timing_read(ast_ctx* ctx, float* out, int n);
+
+/* TensorFlow checkpoint-V2 reader (tf.train.NewCheckpointReader / Saver.restore, methods.py:
+ * 79-84): <prefix>.index (SSTable of BundleEntryProto) + <prefix>.data-NNNNN-of-MMMMM.  Host
+ * memory only, no device.  Entries are in name order; dtype is TF's DataType enum (1 float,
+ * 2 double, 14 bfloat16, 19 half: read as float32; others refused). */
+typedef struct ast_ckpt ast_ckpt;
+int ast_ckpt_open(const char* prefix, ast_ckpt** out);
+void ast_ckpt_close(ast_ckpt* ck);
+int ast_ckpt_num_entries(const ast_ckpt* ck);
+int ast_ckpt_entry(const ast_ckpt* ck, int i, char* name, size_t name_cap, int* dtype, int* ndim,
+                   int64_t* dims, int max_dims);
+int ast_ckpt_read_f32(const ast_ckpt* ck, const char* name, float* host, size_t n);
+/* Saver.restore(sess, prefix) (methods.py:79-84): every encoder variable of the NSynth
+ * checkpoint (ae_startconv, ae_dilatedconv_1..30, ae_res_1..30, ae_bottleneck; W and biases)
+ * by its TF name into ctx, as ast_set_weight.  A missing variable fails with AST_E_NAME. */
+int ast_restore(ast_ctx* ctx, const char* prefix);
 
 /* Batched ADMM optimal transport between NMF palettes: OT_ADMM + transform_palette
  * (optimal_transport.py:77-162; compute_permutation = both).  For each of nprob problems,

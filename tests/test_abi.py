@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, 'include', 'astyle.h')
 def header_functions():
     src = open(HEADER).read()
     src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
-    return sorted(set(re.findall(r'\b(ast_[a-z_]+)\s*\(', src)))
+    return sorted(set(re.findall(r'\b(ast_[a-z0-9_]+)\s*\(', src)))
 
 
 def test_header_and_binding_agree():
