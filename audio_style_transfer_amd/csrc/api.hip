@@ -197,7 +197,7 @@ int plan(const ast_cfg* c, ast_ctx* x) {
         x->gpart_elems = (size_t)c->batch * nch * x->nu * C * C;
         x->smat_elems = (size_t)c->batch * x->nu * C * C;
     } else {
-        nch = std::max(1, c->T / 1024);        // multiples of the stage lengths (16 / 32 rows)
+        nch = std::max(1, c->T / 1024);        // chunks of >= 512 rows: multiples of two split-Gram stages (2 x 16) and of the fp32 / bf16 stages
         x->gpart_elems = (size_t)c->batch * nch * C * 1024;
         x->smat_elems = (size_t)c->batch * C * 1024;
     }

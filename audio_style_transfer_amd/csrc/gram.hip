@@ -13,6 +13,21 @@
 
 namespace ast {
 
+// Work unit of a block: (channel group, (clip, chunk) pair).  Blocks are dispatched to the 8
+// XCDs round-robin, and a 16-channel group reads half of each 128-B line, so the groups sharing
+// lines must share an XCD (and its L2): block id = 8 k + xcd, groups vary with k, pairs with
+// xcd.  (The plain order put the 8 groups of a pair on 8 XCDs and fetched every line twice.)
+__device__ __forceinline__ void gram_unit(int bid, int ncg, int npair, int* cgi, int* pair) {
+    if ((npair & 7) == 0) {
+        const int k = bid >> 3;
+        *cgi = k % ncg;
+        *pair = (k / ncg) * 8 + (bid & 7);
+    } else {
+        *cgi = bid % ncg;
+        *pair = bid / ncg;
+    }
+}
+
 __device__ __forceinline__ f32x16 mfma32g(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -32,10 +47,10 @@ __device__ __forceinline__ void gram_stage(float* Et, const GramArgs& a, int b, 
 __global__ void __launch_bounds__(256) k_gram_fwd(GramArgs a) {
     __shared__ float Et[32 * GLS];
     const int ncg = C / GCH;
-    int bid = blockIdx.x;
-    const int cgi = bid % ncg; bid /= ncg;
-    const int ch = bid % a.nchunk;
-    const int b = bid / a.nchunk;
+    int cgi, pair;
+    gram_unit(blockIdx.x, ncg, a.B * a.nchunk, &cgi, &pair);
+    const int ch = pair % a.nchunk;
+    const int b = pair / a.nchunk;
     const int c0 = cgi * GCH;
     const int tlen = a.T / a.nchunk, tbeg = ch * tlen;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -73,10 +88,10 @@ __global__ void __launch_bounds__(256) k_gram_fwd(GramArgs a) {
 __global__ void __launch_bounds__(256) k_gram_bwd(GramArgs a) {
     __shared__ float Et[32 * GLS];
     const int ncg = C / GCH;
-    int bid = blockIdx.x;
-    const int cgi = bid % ncg; bid /= ncg;
-    const int ch = bid % a.nchunk;
-    const int b = bid / a.nchunk;
+    int cgi, pair;
+    gram_unit(blockIdx.x, ncg, a.B * a.nchunk, &cgi, &pair);
+    const int ch = pair % a.nchunk;
+    const int b = pair / a.nchunk;
     const int c0 = cgi * GCH;
     const int tlen = a.T / a.nchunk, tbeg = ch * tlen;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;

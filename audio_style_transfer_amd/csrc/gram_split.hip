@@ -7,7 +7,8 @@
 // alone, tools/precision_emulate.py).  D leaves in fp32.
 //
 // Per (clip, time chunk, 32-channel group) workgroup, 8 waves x 4 channels, stages of 16 time
-// rows; the next stage's global loads are in flight while a stage computes:
+// rows; the next two stages' global loads (128 KiB per workgroup) are in flight while a stage
+// computes:
 //   fwd  G_c = E_c E_c^T      v_mfma_f32_32x32x16_bf16, A = B fragments (lane (u, h):
 //                             E_u[t0 + 8 h .. + 8][c]) from an LDS image [c][u][hi t | lo t]
 //   bwd  D_c = S~_c E_c       v_mfma_f32_16x16x32_bf16 (A = S~_c halves in registers, B: lane
@@ -81,19 +82,19 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
     for (int cc = 0; cc < 4; ++cc)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[cc][i] = 0.f;
-    float4 v[8];
-    auto load = [&](int t0) {
+    // two stages of loads in flight (v0 / v1 alternate; tlen is a multiple of 2 GSS)
+    float4 v0[8], v1[8];
+    auto load = [&](float4 (&v)[8], int t0) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
     };
-    load(tbeg);
-    for (int t0 = tbeg; t0 < tbeg + tlen; t0 += GSS) {
+    auto stage = [&](float4 (&v)[8], int t0) {
         uint4 fh[4], fl[4];          // channel 4 sq + j: 8 consecutive rows, hi / lo
         split8<0>(v, fh[0], fl[0]);
         split8<1>(v, fh[1], fl[1]);
         split8<2>(v, fh[2], fl[2]);
         split8<3>(v, fh[3], fl[3]);
-        if (t0 + GSS < tbeg + tlen) load(t0 + GSS);     // next stage in flight during this one
+        if (t0 + 2 * GSS < tbeg + tlen) load(v, t0 + 2 * GSS);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -111,6 +112,12 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
             acc[cc] = mfma_bf16(xh, xl, acc[cc]);
             acc[cc] = mfma_bf16(xl, xh, acc[cc]);
         }
+    };
+    load(v0, tbeg);
+    load(v1, tbeg + GSS);
+    for (int t0 = tbeg; t0 < tbeg + tlen; t0 += 2 * GSS) {
+        stage(v0, t0);
+        stage(v1, t0 + GSS);
     }
 #pragma unroll
     for (int cc = 0; cc < 4; ++cc) {
@@ -162,19 +169,19 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
         ld[k] = u < a.nu ? (const float*)a.act + (size_t)a.uid[u] * a.tstride + rowoff : (const float*)a.zero16;
         lrs[k] = u < a.nu ? C : 0;
     }
-    float4 v[8];
-    auto load = [&](int t0) {
+    // two stages of loads in flight (v0 / v1 alternate; tlen is a multiple of 2 GSS)
+    float4 v0[8], v1[8];
+    auto load = [&](float4 (&v)[8], int t0) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (size_t)(t0 + st) * lrs[k]);
     };
-    load(tbeg);
-    for (int t0 = tbeg; t0 < tend; t0 += GSS) {
+    auto stage = [&](float4 (&v)[8], int t0) {
         uint4 fh[4], fl[4];   // channel 4 sq + j: tensors 8 uo .. + 8 at row st, hi / lo
         split8<0>(v, fh[0], fl[0]);
         split8<1>(v, fh[1], fl[1]);
         split8<2>(v, fh[2], fl[2]);
         split8<3>(v, fh[3], fl[3]);
-        if (t0 + GSS < tend) load(t0 + GSS);
+        if (t0 + 2 * GSS < tend) load(v, t0 + 2 * GSS);
         __syncthreads();   // the previous stage's image and O reads are done
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -228,6 +235,12 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
                 }
             }
         }
+    };
+    load(v0, tbeg);
+    load(v1, tbeg + GSS);
+    for (int t0 = tbeg; t0 < tend; t0 += 2 * GSS) {
+        stage(v0, t0);
+        stage(v1, t0 + GSS);
     }
 }
 
