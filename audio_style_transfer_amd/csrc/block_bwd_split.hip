@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     const int r = lane & 31, h = lane >> 5;
     const int G = (int)gridDim.x;
 
-    auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, tiles, a.n, a.d, ly); };
+    auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, a.ft, a.fn, a.d, ly); };
     auto clampt = [&](int tl) { return tl < ntiles ? tl : ntiles - 1; };
 
     // this wave's split weight halves (A: rows = channels 32 w.., K = the other side's channels)
@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         toff[j] = MASKED ? 0 : row_toff(Lc[j], ly, a.d);
     }
     const int chb = 32 * w + 4 * h;
-    auto ctime = [&](const Tile& t, int cc, int to) { return col_time<MASKED>(t, cc, to, a.n, a.d); };
+    auto ctime = [&](const Tile& t, int cc, int to) { return col_time<MASKED>(t, cc, to, a.fn, a.d); };
     // the halo column tile (one-segment layouts): lane r == 0 -> image row 0 (p0 - 1), r == 1 ->
     // row 65 (p0 + 64); lanes r >= 2 compute a copy of row 0 and write it to unused row 66
     const int Lh = r == 1 ? TMS + 1 : 0;
@@ -90,8 +90,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     ru.init(w, lane, ly, a.d);
     float4 lt[NU], lg[NU];
     auto load_unit = [&](const Tile& t, int k) {
-        lt[k] = ru.load(a.tin, t, k, a.T, a.n, a.d);
-        if (HAS_D) lg[k] = ru.load(a.dadd, t, k, a.T, a.n, a.d);
+        lt[k] = ru.load(a.tin, t, k, a.T, a.fn, a.d);
+        if (HAS_D) lg[k] = ru.load(a.dadd, t, k, a.T, a.fn, a.d);
     };
     auto conv_unit = [&](int k, uint8_t* er, float s, uint32_t zb) {
         const float4 v = lt[k];
@@ -148,18 +148,20 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             step3_schedule();
         }
     };
-    // g_u unit (J, g) in two parts: mask + scale; split -> image row
+    // g_u unit (J, g) in two parts: mask; scale + split -> image row
     float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
     auto gu_part = [&](int J, int g, int part, float f) {
         if (part == 0) {
             const uint32_t wd_ = J < 2 ? mu_c[J] : muh_c;
-            gq.x = keep_if(acc1[J][4 * g + 0] * f, wd_, g);
-            gq.y = keep_if(acc1[J][4 * g + 1] * f, wd_, 4 + g);
-            gq.z = keep_if(acc1[J][4 * g + 2] * f, wd_, 8 + g);
-            gq.w = keep_if(acc1[J][4 * g + 3] * f, wd_, 12 + g);
+            gq.x = keep_if(acc1[J][4 * g + 0], wd_, g);
+            gq.y = keep_if(acc1[J][4 * g + 1], wd_, 4 + g);
+            gq.z = keep_if(acc1[J][4 * g + 2], wd_, 8 + g);
+            gq.w = keep_if(acc1[J][4 * g + 3], wd_, 12 + g);
         } else {
+            // the scale after the mask (f is a power of two: the same values), so that the
+            // split's low half fuses with it into one v_fma_mix_f32
             uint2 hi, lo;
-            split4(gq.x, gq.y, gq.z, gq.w, hi, lo);
+            split4(gq.x * f, gq.y * f, gq.z * f, gq.w * f, hi, lo);
             uint8_t* p = XG + (J < 2 ? Lc[J] : Lhw) * RS + 2 * (chb + 8 * g);
             *reinterpret_cast<uint2*>(p) = hi;
             *reinterpret_cast<uint2*>(p + 256) = lo;
@@ -172,7 +174,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         constexpr int J = decltype(j_tag)::value;
         bool ok0 = true, ok2 = true;
         if (MASKED) {
-            const int m = (cu.p0 + 32 * J + r) % a.n;
+            const int pc = cu.p0 + 32 * J + r;
+            const int m = pc - (int)fdiv((uint32_t)pc, a.fn) * a.n;
             ok0 = m > 0;
             ok2 = m < a.n - 1;
         }
@@ -241,7 +244,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
 #pragma unroll
         for (int k = 0; k < NU; ++k) load_unit(t0, k);
         load_masks(t0, mu_c, muh_c, me_c);
-        const uint32_t z0 = ru.zero_bits(t0, a.n);
+        const uint32_t z0 = ru.zero_bits(t0, a.fn);
         const float s0 = exp2i(scale_exp(sload(a.gmax_in + t0.b)));
 #pragma unroll
         for (int k = 0; k < NU; ++k) conv_unit(k, &ER[0][0], s0, z0);
@@ -266,7 +269,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         const float f_u = exp2i(m_u - m_t - a.kr);   // acc units 2^(m_t + k_r) -> g_u 2^m_u
         const float inv2 = exp2i(-(m_u + a.kd));
         const float s_next = exp2i(scale_exp(sload(a.gmax_in + nt.b)));
-        const uint32_t zn = ru.zero_bits(nt, a.n);
+        const uint32_t zn = ru.zero_bits(nt, a.fn);
         uint8_t* erc = &ER[it & 1][0];          // this tile's residual
         uint8_t* ero = &ER[(it & 1) ^ 1][0];    // the previous tile's, then the next tile's
 
@@ -345,7 +348,10 @@ __global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, siz
 
 }  // namespace
 
-void launch_block_bwd_s(const BwdArgsS& a, hipStream_t s) {
+void launch_block_bwd_s(const BwdArgsS& a0, hipStream_t s) {
+    BwdArgsS a = a0;
+    a.fn = make_fdiv((uint32_t)a.n);
+    a.ft = make_fdiv((uint32_t)(a.T / TMS));
     const int nt = a.B * (a.T / TMS);
     const dim3 grid(std::min(nt, sw::num_cus()));
     Layout ly;

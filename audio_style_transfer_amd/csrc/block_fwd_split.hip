@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     const int r = lane & 31, h = lane >> 5;
     const int G = (int)gridDim.x;
 
-    auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, tiles, a.n, a.d, ly); };
+    auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, a.ft, a.fn, a.d, ly); };
     // tiles past the end repeat the last one (loaded and converted, never used)
     auto clampt = [&](int tl) { return tl < ntiles ? tl : ntiles - 1; };
 
@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         toff[j] = MASKED ? 0 : row_toff(Lc[j], ly, a.d);
     }
     const int chb = 32 * w + 4 * h;   // first channel of this lane's accumulator group g = 0
-    auto ctime = [&](const Tile& t, int cc, int to) { return col_time<MASKED>(t, cc, to, a.n, a.d); };
+    auto ctime = [&](const Tile& t, int cc, int to) { return col_time<MASKED>(t, cc, to, a.fn, a.d); };
 
     // ---- row units: unit k, lane -> image row L = 8 k + lr, channels cq .. cq + 3 ----
     const int lr = lane >> 3;
@@ -105,22 +105,21 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         if (MASKED) {
             const int L = 8 * k + lr;
             const int pp = t.p0 + ((padz >> k) & 1u ? 0 : L - 1);
-            const float* src = a.ein + ((size_t)t.b * a.T + (pp % a.n) * a.d + pp / a.n) * C + cq;
+            const float* src = a.ein + ((size_t)t.b * a.T + pos_time(pp, a.fn, a.d)) * C + cq;
             ld[k] = *reinterpret_cast<const float4*>(src);
             return;
         }
         const char* base = reinterpret_cast<const char*>(a.ein + ((ptrdiff_t)t.b * a.T + t.tb - a.d) * C);
         uint32_t o = soff[k];
-        if (ONESEG && k == 0 && lr == 0 && t.p0 % a.n == 0) o = row1;
-        if (ONESEG && k == NU - 1 && lr == 1 && t.p0 % a.n + TMS >= a.n) o = row64;
+        if (ONESEG && k == 0 && lr == 0 && t.m0 == 0) o = row1;
+        if (ONESEG && k == NU - 1 && lr == 1 && t.m0 + TMS >= a.n) o = row64;
         ld[k] = *reinterpret_cast<const float4*>(base + o);
     };
     auto zero_bits_of = [&](const Tile& t) {
         uint32_t z = padz;
         if (ONESEG) {
-            const int m0 = t.p0 % a.n;
-            if (lr == 0 && m0 == 0) z |= 1u;
-            if (lr == 1 && m0 + TMS >= a.n) z |= 1u << (NU - 1);
+            if (lr == 0 && t.m0 == 0) z |= 1u;
+            if (lr == 1 && t.m0 + TMS >= a.n) z |= 1u << (NU - 1);
         }
         return z;
     };
@@ -180,8 +179,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         } else {
             emax = fmaxf(emax, fmaxf(fmaxf(fabsf(e2o.x), fabsf(e2o.y)), fmaxf(fabsf(e2o.z), fabsf(e2o.w))));
             // bit mbit(4 g + q) = 4 q + g of the column's word (common.h)
-            mb[j] |= pos_bit(e2o.x) << g | pos_bit(e2o.y) << (4 + g) | pos_bit(e2o.z) << (8 + g) |
-                     pos_bit(e2o.w) << (12 + g);
+            mb[j] = or_pos_bits4(mb[j], e2o.x, e2o.y, e2o.z, e2o.w, g);
         }
     };
     // words and column times to LDS (all lanes write: identical values per column)
@@ -210,8 +208,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             e1u.y = fmaf(acc1[j][4 * g + 1], inv1, b4.y);
             e1u.z = fmaf(acc1[j][4 * g + 2], inv1, b4.z);
             e1u.w = fmaf(acc1[j][4 * g + 3], inv1, b4.w);
-            mu_w |= pos_bit(e1u.x) << g | pos_bit(e1u.y) << (4 + g) | pos_bit(e1u.z) << (8 + g) |
-                    pos_bit(e1u.w) << (12 + g);
+            mu_w = or_pos_bits4(mu_w, e1u.x, e1u.y, e1u.z, e1u.w, g);
         } else {
             uint2 hi, lo;
             split4(fmaxf(e1u.x, 0.f) * sv, fmaxf(e1u.y, 0.f) * sv, fmaxf(e1u.z, 0.f) * sv,
@@ -231,7 +228,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         constexpr int J = decltype(j_tag)::value;
         bool ok0 = true, ok2 = true;
         if (MASKED) {
-            const int m = (cu.p0 + 32 * J + r) % a.n;
+            const int pc = cu.p0 + 32 * J + r;
+            const int m = pc - (int)fdiv((uint32_t)pc, a.fn) * a.n;
             ok0 = m > 0;
             ok2 = m < a.n - 1;
         }
@@ -398,7 +396,10 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
 
 }  // namespace
 
-void launch_block_fwd_s(const FwdArgsS& a, hipStream_t s) {
+void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
+    FwdArgsS a = a0;
+    a.fn = make_fdiv((uint32_t)a.n);
+    a.ft = make_fdiv((uint32_t)(a.T / TMS));
     const int nt = a.B * (a.T / TMS);
     const dim3 grid(std::min(nt, sw::num_cus()));
     Layout ly;

@@ -26,10 +26,6 @@ namespace ast {
 constexpr int C = 128;
 constexpr int TM = 64;        // rows per encoder tile
 constexpr int XS = 130;       // LDS row stride (floats): ds_read_b64 conflict-free
-constexpr int GT = 32;        // Gram: time rows per stage
-constexpr int GCH = 16;       // Gram: channels per workgroup
-constexpr int GRS = 17;       // Gram LDS row stride (floats)
-constexpr int GLS = GT * GRS + 1;   // Gram LDS layer stride (545: odd -> conflict-free)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned short u16;                 // raw bf16 storage
@@ -160,6 +156,26 @@ struct BwdArgsC {
 //   wrb [4 w][8 kb][2 hl][64]:                                     W_r[32 w + m][16 kb + 8 h + e]
 //   wdb [4 w][3 tap][8 kb][2 hl][64]:                              W_d[tap][32 w + m][16 kb + 8 h + e]
 // gmax_*: per clip max |x| of a tensor as float bits (atomic max of the non-negative bit pattern).
+// Division by a launch-invariant divisor without the signed-division expansion (~17 scalar
+// instructions each): q = mulhi(x, m) >> s with m = ceil(2^(31 + l) / n), 2^l >= n, exact for
+// every 0 <= x < 2^31 (Granlund-Montgomery); n = 1 passes x through.
+struct FDiv {
+    uint32_t n, m, s;
+};
+inline FDiv make_fdiv(uint32_t n) {
+    FDiv f{n, 0u, 0u};
+    if (n > 1) {
+        uint32_t l = 0;
+        while ((1ull << l) < n) ++l;
+        f.m = (uint32_t)(((1ull << (31 + l)) + n - 1) / n);
+        f.s = l - 1;
+    }
+    return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FDiv& f) {
+    return f.n == 1 ? x : __umulhi(x, f.m) >> f.s;
+}
+
 struct FwdArgsS {
     unsigned long long* stamps;            // diagnostic builds (-DASTYLE_STAMPS) only
     const float* ein; float* eout;
@@ -174,6 +190,7 @@ struct FwdArgsS {
     int dn_log2, nn;       // next layer: log2 dilation, T / dilation
     int kd, kr;            // weight exponents
     float wdn, bdm;        // max_co sum_{tap,ci} |W_d|, max |b_d|: |u| <= wdn max|e_l| + bdm
+    FDiv fn, ft;           // by n, by tiles per clip (T / 64): set by the launcher
 };
 
 struct BwdArgsS {
@@ -189,6 +206,7 @@ struct BwdArgsS {
     int B, T, d, n;
     int kd, kr;
     float wrn;             // max_ci sum_co |W_r|: |W_r tot| <= wrn max|tot|
+    FDiv fn, ft;           // by n, by tiles per clip (T / 64): set by the launcher
 };
 
 struct GramArgs {

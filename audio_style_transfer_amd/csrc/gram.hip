@@ -1,147 +1,11 @@
 // Channel-wise ("ours") Gram, l2-normalise, style/content losses and their gradients
 // (methods.py:58-76, 113-125) on gfx950.
 //
-// Gram fwd: G_c[u][u'] = sum_t E_u[t][c] E_u'[t][c] for the U unique tapped tensors, one
-//   v_mfma_f32_32x32x2_f32 per (channel, 2 time steps) with A = B = the same register
-//   (lane (i,h) holds E_i[t0+2s+h][c]); partial sums per time chunk, no atomics.
-// Gram bwd: D_u[t][c] = sum_u' S~_c[u][u'] E_u'[t][c] (+ content grad), S~ = dG + dG^T folded
-//   onto unique tensors; written in place over E_u (E is dead after this pass: the backward
-//   chain uses the mask bits).
-// Both stage a [32 tensors][32 t][16 ch] fp32 tile in LDS (layer stride 545, row stride 17:
-// both the row-indexed and the column-indexed operand reads are bank-conflict free).
+// The fp32 Gram kernels themselves (fwd G_c = E_c E_c^T, bwd D_c = S~_c E_c in place over E)
+// are in gram_split.hip beside the split ones, which share their staging.
 #include "common.h"
 
 namespace ast {
-
-// Work unit of a block: (channel group, (clip, chunk) pair).  Blocks are dispatched to the 8
-// XCDs round-robin, and a 16-channel group reads half of each 128-B line, so the groups sharing
-// lines must share an XCD (and its L2): block id = 8 k + xcd, groups vary with k, pairs with
-// xcd.  (The plain order put the 8 groups of a pair on 8 XCDs and fetched every line twice.)
-__device__ __forceinline__ void gram_unit(int bid, int ncg, int npair, int* cgi, int* pair) {
-    if ((npair & 7) == 0) {
-        const int k = bid >> 3;
-        *cgi = k % ncg;
-        *pair = (k / ncg) * 8 + (bid & 7);
-    } else {
-        *cgi = bid % ncg;
-        *pair = bid / ncg;
-    }
-}
-
-__device__ __forceinline__ f32x16 mfma32g(float a, float b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ void gram_stage(float* Et, const GramArgs& a, int b, int t0, int c0,
-                                           int tid) {
-    for (int i = tid; i < a.nu * GT * 4; i += 256) {
-        const int u = i / (GT * 4), rem = i - u * (GT * 4);
-        const int tt = rem >> 2, q = rem & 3;
-        const float4 v = *reinterpret_cast<const float4*>(
-            (const float*)a.act + (size_t)a.uid[u] * a.tstride + ((size_t)b * a.T + t0 + tt) * C + c0 + q * 4);
-        float* dst = &Et[u * GLS + tt * GRS + q * 4];
-        dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
-    }
-}
-
-__global__ void __launch_bounds__(256) k_gram_fwd(GramArgs a) {
-    __shared__ float Et[32 * GLS];
-    const int ncg = C / GCH;
-    int cgi, pair;
-    gram_unit(blockIdx.x, ncg, a.B * a.nchunk, &cgi, &pair);
-    const int ch = pair % a.nchunk;
-    const int b = pair / a.nchunk;
-    const int c0 = cgi * GCH;
-    const int tlen = a.T / a.nchunk, tbeg = ch * tlen;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r = lane & 31, h = lane >> 5;
-    for (int i = a.nu * GLS + tid; i < 32 * GLS; i += 256) Et[i] = 0.f;
-
-    f32x16 acc[4];
-    for (int cc = 0; cc < 4; ++cc)
-        for (int i = 0; i < 16; ++i) acc[cc][i] = 0.f;
-    for (int t0 = tbeg; t0 < tbeg + tlen; t0 += GT) {
-        __syncthreads();
-        gram_stage(Et, a, b, t0, c0, tid);
-        __syncthreads();
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-            const int c = w * 4 + cc;
-#pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                const float v = Et[r * GLS + (2 * s + h) * GRS + c];
-                acc[cc] = mfma32g(v, v, acc[cc]);
-            }
-        }
-    }
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
-        float* dst = a.gpart + (((size_t)b * a.nchunk + ch) * C + c0 + w * 4 + cc) * 1024;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int R = (i & 3) + 8 * (i >> 2) + 4 * h;
-            dst[R * 32 + r] = acc[cc][i];
-        }
-    }
-}
-
-__global__ void __launch_bounds__(256) k_gram_bwd(GramArgs a) {
-    __shared__ float Et[32 * GLS];
-    const int ncg = C / GCH;
-    int cgi, pair;
-    gram_unit(blockIdx.x, ncg, a.B * a.nchunk, &cgi, &pair);
-    const int ch = pair % a.nchunk;
-    const int b = pair / a.nchunk;
-    const int c0 = cgi * GCH;
-    const int tlen = a.T / a.nchunk, tbeg = ch * tlen;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r = lane & 31, h = lane >> 5;
-    for (int i = a.nu * GLS + tid; i < 32 * GLS; i += 256) Et[i] = 0.f;
-
-    // A fragments: S~_c[i = r][k = 2s + h] for this wave's 4 channels
-    float sa[4][16];
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
-        const float* sm = a.smat + ((size_t)b * C + c0 + w * 4 + cc) * 1024 + r * 32 + h;
-#pragma unroll
-        for (int s = 0; s < 16; ++s) sa[cc][s] = sm[2 * s];
-    }
-    for (int t0 = tbeg; t0 < tbeg + tlen; t0 += GT) {
-        __syncthreads();
-        gram_stage(Et, a, b, t0, c0, tid);
-        __syncthreads();
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-            const int c = w * 4 + cc;
-            f32x16 acc;
-            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-            for (int s = 0; s < 16; ++s)
-                acc = mfma32g(sa[cc][s], Et[(2 * s + h) * GLS + r * GRS + c], acc);
-            // this wave alone reads/writes column c: overwrite E with D in place
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int R = (i & 3) + 8 * (i >> 2) + 4 * h;
-                Et[R * GLS + r * GRS + c] = acc[i];
-            }
-        }
-        __syncthreads();
-        for (int i = tid; i < a.nu * GT * 4; i += 256) {
-            const int u = i / (GT * 4), rem = i - u * (GT * 4);
-            const int tt = rem >> 2, q = rem & 3;
-            const size_t o = (size_t)a.uid[u] * a.tstride + ((size_t)b * a.T + t0 + tt) * C + c0 + q * 4;
-            const float* src = &Et[u * GLS + tt * GRS + q * 4];
-            float4 v = make_float4(src[0], src[1], src[2], src[3]);
-            const float* cgp = (const float*)a.cg[u];
-            if (cgp) {
-                const float4 g = *reinterpret_cast<const float4*>(
-                    cgp + ((size_t)b * a.T + t0 + tt) * C + c0 + q * 4);
-                v.x += g.x; v.y += g.y; v.z += g.z; v.w += g.w;
-            }
-            *reinterpret_cast<float4*>((float*)a.actw + o) = v;
-        }
-    }
-}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -346,12 +210,6 @@ __global__ void __launch_bounds__(256) k_finalize(float* parts, const float* cpa
     }
 }
 
-void launch_gram_fwd(const GramArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_gram_fwd, dim3(a.B * a.nchunk * (C / GCH)), dim3(256), 0, s, a);
-}
-void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_gram_bwd, dim3(a.B * a.nchunk * (C / GCH)), dim3(256), 0, s, a);
-}
 void launch_style_ours(const StyleArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_style_ours, dim3(a.B * (C / 4)), dim3(256), 0, s, a);
 }

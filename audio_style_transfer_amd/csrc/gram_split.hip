@@ -1,5 +1,6 @@
-// Channel-wise ("ours") Gram forward/backward on bf16 MFMA over fp32 activations (precision 2),
-// methods.py:62-76.  The activations stay fp32 in HBM.  Each Gram operand is carried as two
+// Channel-wise ("ours") Gram forward/backward, methods.py:62-76: on bf16 MFMA over fp32
+// activations (precision 2, *_s kernels) and on fp32 MFMA (precision 0, *_f kernels, the same
+// staging).  The activations stay fp32 in HBM.  Each Gram operand is carried as two
 // bf16 terms, x ~ xh + xl (xh = bf16(x), xl = bf16(x - xh)), and every product as
 // xh yh + xh yl + xl yh on v_mfma_*_bf16 with fp32 accumulation: the Gram is HBM-bound (10
 // flop/B), so the three products cost no time, and they keep the gradient at fp32-class error
@@ -244,10 +245,205 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     }
 }
 
+// ---- fp32 mode (precision 0): the same staging and data movement on fp32 MFMA ----
+// forward: image [c][u][t] fp32 (row stride FRF floats: 80 B, conflict-free reads); lane (r, h)
+// reads E_r[t0 + 8 h .. + 8][c] (two 16-B reads) and runs 8 v_mfma_f32_32x32x2f32 with A = B
+// = that value (k-step s takes time 8 h + s: any common permutation of K is the same Gram).
+constexpr int FRF = 20;
+__device__ __forceinline__ f32x16 mfma_f32_32(float a, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, a, c, 0, 0, 0);
+}
+
+__global__ void __launch_bounds__(GWT) k_gram_fwd_f(GramArgs a) {
+    __shared__ __attribute__((aligned(16))) float I[GCS * 32 * FRF];   // [c][u][t]
+    int b, ch, c0;
+    decode(a, b, ch, c0);
+    const int tlen = a.T / a.nchunk, tbeg = ch * tlen;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int su = 8 * (w & 3) + (lane & 7), sq = lane >> 3, tb = w >> 2;
+    const bool real = su < a.nu;
+    const float* src = real ? (const float*)a.act + (size_t)a.uid[su] * a.tstride +
+                              (size_t)b * a.T * C + c0 + 4 * sq + (size_t)8 * tb * C
+                            : (const float*)a.zero16;
+    const size_t rs = real ? C : 0;
+    f32x16 acc[4];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[cc][i] = 0.f;
+    float4 v0[8], v1[8];
+    auto load = [&](float4 (&v)[8], int t0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
+    };
+    auto stage = [&](float4 (&v)[8], int t0) {
+        float4 f[4][2];   // channel 4 sq + j: rows 8 tb .. + 8
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            auto e = [&](int k) { return j == 0 ? v[k].x : j == 1 ? v[k].y : j == 2 ? v[k].z : v[k].w; };
+            f[j][0] = make_float4(e(0), e(1), e(2), e(3));
+            f[j][1] = make_float4(e(4), e(5), e(6), e(7));
+        }
+        if (t0 + 2 * GSS < tbeg + tlen) load(v, t0 + 2 * GSS);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float* row = &I[((4 * sq + j) * 32 + su) * FRF + 8 * tb];
+            *reinterpret_cast<float4*>(row) = f[j][0];
+            *reinterpret_cast<float4*>(row + 4) = f[j][1];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const float* row = &I[((4 * w + cc) * 32 + r) * FRF + 8 * h];
+            const float4 p = *reinterpret_cast<const float4*>(row);
+            const float4 q = *reinterpret_cast<const float4*>(row + 4);
+            acc[cc] = mfma_f32_32(p.x, acc[cc]);
+            acc[cc] = mfma_f32_32(p.y, acc[cc]);
+            acc[cc] = mfma_f32_32(p.z, acc[cc]);
+            acc[cc] = mfma_f32_32(p.w, acc[cc]);
+            acc[cc] = mfma_f32_32(q.x, acc[cc]);
+            acc[cc] = mfma_f32_32(q.y, acc[cc]);
+            acc[cc] = mfma_f32_32(q.z, acc[cc]);
+            acc[cc] = mfma_f32_32(q.w, acc[cc]);
+        }
+    };
+    load(v0, tbeg);
+    load(v1, tbeg + GSS);
+    for (int t0 = tbeg; t0 < tbeg + tlen; t0 += 2 * GSS) {
+        stage(v0, t0);
+        stage(v1, t0 + GSS);
+    }
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+        float* dst = a.gpart + (((size_t)b * a.nchunk + ch) * C + c0 + 4 * w + cc) * 1024;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dst[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = acc[cc][i];
+    }
+}
+
+// backward: image [c][t][u] fp32, 32 floats per row with the four 8-tensor blocks swizzled
+// (block kq of row t at 8 (kq ^ (t & 3)): conflict-free 16-B reads); D_c = S~_c E_c on
+// v_mfma_f32_16x16x4f32: A = S~_c[u = 16 m + i16][u' = 8 kq + ks] in registers, B: lane
+// (t = i16, kq) reads E_{8 kq .. + 8}[t][c] (two 16-B reads), k-step ks.  Output as the split
+// kernel's (O image, whole 128-B lines, in place over E, + the content grad).
+__device__ __forceinline__ int bswz(int kq, int t) { return 8 * (kq ^ (t & 3)); }
+
+__global__ void __launch_bounds__(GWT) k_gram_bwd_f(GramArgs a) {
+    __shared__ __attribute__((aligned(16))) float IB[GCS * GSS * 32];     // [c][t][u]
+    __shared__ __attribute__((aligned(16))) float O[16 * GSS * ORS];      // [u][t][c]
+    int b, ch, c0;
+    decode(a, b, ch, c0);
+    const int tlen = a.T / a.nchunk, tbeg = ch * tlen, tend = tbeg + tlen;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int i16 = lane & 15, kq = lane >> 4;
+    float sa[4][2][8];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const float* sm = a.smat + ((size_t)b * C + c0 + 4 * w + cc) * 1024 + (16 * m + i16) * 32 + 8 * kq;
+            const float4 p = *reinterpret_cast<const float4*>(sm);
+            const float4 q = *reinterpret_cast<const float4*>(sm + 4);
+            sa[cc][m][0] = p.x; sa[cc][m][1] = p.y; sa[cc][m][2] = p.z; sa[cc][m][3] = p.w;
+            sa[cc][m][4] = q.x; sa[cc][m][5] = q.y; sa[cc][m][6] = q.z; sa[cc][m][7] = q.w;
+        }
+    const int uo = w & 3, sq = lane >> 3, st = 8 * (w >> 2) + (lane & 7);
+    const size_t rowoff = (size_t)b * a.T * C + c0 + 4 * sq;
+    const float* ld[8];
+    size_t lrs[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int u = 8 * uo + k;
+        ld[k] = u < a.nu ? (const float*)a.act + (size_t)a.uid[u] * a.tstride + rowoff : (const float*)a.zero16;
+        lrs[k] = u < a.nu ? C : 0;
+    }
+    float4 v0[8], v1[8];
+    auto load = [&](float4 (&v)[8], int t0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (size_t)(t0 + st) * lrs[k]);
+    };
+    auto stage = [&](float4 (&v)[8], int t0) {
+        float4 f[4][2];   // channel 4 sq + j: tensors 8 uo .. + 8 at row st
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            auto e = [&](int k) { return j == 0 ? v[k].x : j == 1 ? v[k].y : j == 2 ? v[k].z : v[k].w; };
+            f[j][0] = make_float4(e(0), e(1), e(2), e(3));
+            f[j][1] = make_float4(e(4), e(5), e(6), e(7));
+        }
+        if (t0 + 2 * GSS < tend) load(v, t0 + 2 * GSS);
+        __syncthreads();   // the previous stage's image and O reads are done
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float* row = &IB[((4 * sq + j) * GSS + st) * 32 + bswz(uo, st)];
+            *reinterpret_cast<float4*>(row) = f[j][0];
+            *reinterpret_cast<float4*>(row + 4) = f[j][1];
+        }
+        __syncthreads();
+        f32x4 acc[4][2];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const float* row = &IB[((4 * w + cc) * GSS + i16) * 32 + bswz(kq, i16)];
+            const float4 p = *reinterpret_cast<const float4*>(row);
+            const float4 q = *reinterpret_cast<const float4*>(row + 4);
+            const float bv[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 8; ++ks)
+                    c = __builtin_amdgcn_mfma_f32_16x16x4f32(sa[cc][m][ks], bv[ks], c, 0, 0, 0);
+                acc[cc][m] = c;
+            }
+        }
+        // lane holds D_c[u = 16 m + 4 kq + i][t = i16] for the wave's 4 channels
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            if (m) __syncthreads();   // the first half's O reads are done
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    O[((4 * kq + i) * GSS + i16) * ORS + 4 * w + cc] = acc[cc][m][i];
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int pp = it * GWT + tid;
+                const int ul = pp >> 7, tt = (pp >> 3) & 15, q = pp & 7;
+                const int u = 16 * m + ul;
+                if (u < a.nu) {
+                    float4 o = *reinterpret_cast<const float4*>(&O[(ul * GSS + tt) * ORS + 4 * q]);
+                    const size_t off = (size_t)a.uid[u] * a.tstride + ((size_t)b * a.T + t0 + tt) * C + c0 + 4 * q;
+                    const float* cg = (const float*)a.cg[u];
+                    if (cg) {
+                        const float4 g = *reinterpret_cast<const float4*>(cg + ((size_t)b * a.T + t0 + tt) * C + c0 + 4 * q);
+                        o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
+                    }
+                    *reinterpret_cast<float4*>((float*)a.actw + off) = o;
+                }
+            }
+        }
+    };
+    load(v0, tbeg);
+    load(v1, tbeg + GSS);
+    for (int t0 = tbeg; t0 < tend; t0 += 2 * GSS) {
+        stage(v0, t0);
+        stage(v1, t0 + GSS);
+    }
+}
+
 }  // namespace
 
 void launch_gram_fwd_s(const GramArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gram_fwd_s, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+}
+void launch_gram_fwd(const GramArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_gram_fwd_f, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+}
+void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_gram_bwd_f, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
 void launch_gram_bwd_s(const GramArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gram_bwd_s, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
