@@ -22,7 +22,7 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall',
 # MFMA accumulators in arch VGPRs, where the epilogues read them without copies; their fully
 # unrolled tile loops exceed the default pragma-unroll size limit (a partly unrolled loop would
 # index the register-resident weight arrays dynamically and demote them to scratch)
-_CW = ['-mllvm', '-amdgpu-mfma-vgpr-form=1', '-mllvm', '-pragma-unroll-threshold=1000000', '-fno-slp-vectorize']
+_CW = ['-mllvm', '-amdgpu-mfma-vgpr-form=1', '-mllvm', '-amdgpu-atomic-optimizer-strategy=None', '-mllvm', '-pragma-unroll-threshold=1000000', '-fno-slp-vectorize']
 EXTRA = {'block_fwd_bf16.hip': _CW, 'block_bwd_bf16.hip': _CW, 'block_fwd_split.hip': _CW,
          'block_bwd_split.hip': _CW}
 
@@ -41,10 +41,15 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, exp:
     (drops parts of their work; results are wrong) -> libastyle_stamps_exp<exp>.so"""
     tag = '' if not exp else '_exp%d' % exp
     lib = LIB if not stamps else os.path.join(PKG, 'libastyle_stamps%s.so' % tag)
-    if not force and not stamps and not _stale():
+    variant = os.environ.get('ASTYLE_VARIANT', '')   # A/B builds: libastyle_<variant>.so
+    defs = os.environ.get('ASTYLE_DEFS', '').split()
+    if variant:
+        lib = os.path.join(PKG, 'libastyle_%s.so' % variant)
+        stamps = stamps or False
+    if not force and not stamps and not variant and not _stale():
         return LIB
-    objdir = os.path.join(PKG, 'build' if not stamps else 'build_stamps' + tag)
-    flags = FLAGS + (['-DASTYLE_STAMPS'] if stamps else []) + (['-DSW_EXP=%d' % exp] if exp else [])
+    objdir = os.path.join(PKG, 'build_' + variant if variant else 'build' if not stamps else 'build_stamps' + tag)
+    flags = FLAGS + (['-DASTYLE_STAMPS'] if stamps else []) + (['-DSW_EXP=%d' % exp] if exp else []) + defs
     os.makedirs(objdir, exist_ok=True)
 
     def cc(src):

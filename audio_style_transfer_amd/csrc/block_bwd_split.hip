@@ -222,14 +222,16 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             oo.y = fmaf(keep_if(acc2[J][4 * g + 1], mw, 4 + g), inv2, oe.y);
             oo.z = fmaf(keep_if(acc2[J][4 * g + 2], mw, 8 + g), inv2, oe.z);
             oo.w = fmaf(keep_if(acc2[J][4 * g + 3], mw, 12 + g), inv2, oe.w);
+#if !(defined(SW_EXP) && SW_EXP == 8)
             *reinterpret_cast<float4*>(dst + 8 * g) = oo;
+#endif
         } else {
             omax = fmaxf(omax, fmaxf(fmaxf(fabsf(oo.x), fabsf(oo.y)), fmaxf(fabsf(oo.z), fabsf(oo.w))));
         }
     };
     auto epi_max = [&](int b) {
-        const float m = wave_max(omax);
-        if (lane == 0) atomicMax(a.gmax_out + b, __float_as_uint(m));
+        const uint32_t m = wave_max_bits(omax);
+        if (lane == 0) atomicMax(a.gmax_out + b, m);
         omax = 0.f;
     };
     using J0 = std::integral_constant<int, 0>;
@@ -239,13 +241,15 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     if (blockIdx.x >= ntiles) return;   // (grid = min(tiles, CUs): not taken)
 
     // prologue: the first tile's image, residual rows and masks; the second tile's rows in flight
+    float gm_c;     // max |tot| of the current tile's clip (one scalar load per tile: the next one's)
     {
         const Tile t0 = tile_of(blockIdx.x);
 #pragma unroll
         for (int k = 0; k < NU; ++k) load_unit(t0, k);
         load_masks(t0, mu_c, muh_c, me_c);
         const uint32_t z0 = ru.zero_bits(t0, a.fn);
-        const float s0 = exp2i(scale_exp(sload(a.gmax_in + t0.b)));
+        gm_c = sload(a.gmax_in + t0.b);
+        const float s0 = exp2i(scale_exp(gm_c));
 #pragma unroll
         for (int k = 0; k < NU; ++k) conv_unit(k, &ER[0][0], s0, z0);
         const Tile t1 = tile_of(clampt(blockIdx.x + G));
@@ -263,16 +267,18 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         // T: this tile's tot image complete (converted during the previous phase C)
         lds_barrier();
         STAMP(6)
-        const float gm = sload(a.gmax_in + cu.b);
+        const float gm = gm_c;
         const int m_t = scale_exp(gm);
         const int m_u = scale_exp(a.wrn * gm);
         const float f_u = exp2i(m_u - m_t - a.kr);   // acc units 2^(m_t + k_r) -> g_u 2^m_u
         const float inv2 = exp2i(-(m_u + a.kd));
-        const float s_next = exp2i(scale_exp(sload(a.gmax_in + nt.b)));
+        gm_c = sload(a.gmax_in + nt.b);
+        const float s_next = exp2i(scale_exp(gm_c));
         const uint32_t zn = ru.zero_bits(nt, a.fn);
         uint8_t* erc = &ER[it & 1][0];          // this tile's residual
         uint8_t* ero = &ER[(it & 1) ^ 1][0];    // the previous tile's, then the next tile's
 
+        STAMP(11)
         // A: g_v half 0 + epilogue half 1 of the previous tile (parts 0..7)
         if (!FIRST) epi_begin(prv, 1);
         gemm1(J0{}, [&](int kb) { if (!FIRST) epi_part(1, kb / 3, kb % 3, ero, me_p, inv2p); });
@@ -299,7 +305,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         gemm2(J0{}, [&](int st) {
             if (st < NU) {
                 conv_unit(st, ero, s_next, zn);
+#if !(defined(SW_EXP) && SW_EXP == 9)
                 load_unit(n2, st);
+#endif
             }
             if (st == NU) load_masks(nt, mu_n, muh_n, me_n);
         }, cu);

@@ -32,6 +32,12 @@ using namespace sw;
 constexpr int IROWS = 72;             // image / residual rows: 66 or 68 used, 9 units x 8 rows
 constexpr int ISLOT = IROWS * RS;     // bytes per image / residual buffer
 constexpr int LA = 2;                 // B-fragment lookahead (steps)
+#ifndef FWD_FLUSH
+#define FWD_FLUSH 1                   // epilogue 2 rows leave through LDS as whole lines (else direct)
+#endif
+#ifndef FWD_LOAD_AB
+#define FWD_LOAD_AB 1                 // next tile's row loads in phases A / B (else D, two tiles ahead)
+#endif
 
 template <bool MASKED, bool ONESEG>
 __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
@@ -148,22 +154,22 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         }
     };
 
-    // ---- epilogue 2 of tile prv (residual rows erp), unit u = (j, g) in three parts ----
+    // ---- epilogue 2 of tile prv (residual rows erp), unit u = (j, g) in three parts.  e_{l+1}
+    //      goes back into the residual rows it was computed from (in place: only this wave reads
+    //      its quarter), and leaves for HBM from there as whole 128-B lines (flush: 8 columns x
+    //      the wave's 32 channels per store); stored straight from the accumulator layout, each
+    //      store would touch 32 lines 32 B at a time ----
     f32x16 acc2[2];                    // y of the pending epilogue 2
     Tile prv = tile_of(blockIdx.x);
     float inv2p = 0.f;
     float emax = 0.f;
     uint32_t mb[2] = {0u, 0u};
-    float* dstj[2] = {nullptr, nullptr};
     float4 e2e, e2b, e2o;
     auto epi2_begin = [&]() {
         emax = 0.f;
         mb[0] = mb[1] = 0u;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            dstj[j] = a.eout + ((size_t)prv.b * a.T + ctime(prv, 32 * j + r, toff[j])) * C + chb;
     };
-    auto epi2_part = [&](int u, int part, const uint8_t* erp) {
+    auto epi2_part = [&](int u, int part, uint8_t* erp) {
         const int j = u >> 2, g = u & 3;
         if (part == 0) {
             e2e = *reinterpret_cast<const float4*>(erp + Lc[j] * RS + 4 * (chb + 8 * g));
@@ -173,13 +179,30 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             e2o.y = e2e.y + fmaf(acc2[j][4 * g + 1], inv2p, e2b.y);
             e2o.z = e2e.z + fmaf(acc2[j][4 * g + 2], inv2p, e2b.z);
             e2o.w = e2e.w + fmaf(acc2[j][4 * g + 3], inv2p, e2b.w);
-#if !(defined(SW_EXP) && SW_EXP == 8)
-            *reinterpret_cast<float4*>(dstj[j] + 8 * g) = e2o;
+#if FWD_FLUSH
+            *reinterpret_cast<float4*>(erp + Lc[j] * RS + 4 * (chb + 8 * g)) = e2o;
+#else
+            *reinterpret_cast<float4*>(a.eout + ((size_t)prv.b * a.T + ctime(prv, 32 * j + r, toff[j])) * C + chb + 8 * g) = e2o;
 #endif
         } else {
             emax = fmaxf(emax, fmaxf(fmaxf(fabsf(e2o.x), fabsf(e2o.y)), fmaxf(fabsf(e2o.z), fabsf(e2o.w))));
             // bit mbit(4 g + q) = 4 q + g of the column's word (common.h)
             mb[j] = or_pos_bits4(mb[j], e2o.x, e2o.y, e2o.z, e2o.w, g);
+        }
+    };
+    // flush piece (j, q): columns 32 j + 8 q + lr (lr = lane >> 3), channels cq .. cq + 3; part 0
+    // reads the row back, part 1 stores it
+    float4 fl4;
+    auto flush_part = [&](int j, int q, int part, const uint8_t* erp) {
+        if (!FWD_FLUSH) return;
+        const int c = 32 * j + 8 * q + lr;
+        if (part == 0) {
+            const int row = (MASKED || ONESEG) ? c + 1 : 34 * j + 1 + 8 * q + lr;   // frow(c)
+            fl4 = *reinterpret_cast<const float4*>(erp + row * RS + 4 * cq);
+        } else {
+            const int t = MASKED ? pos_time(prv.p0 + c, a.fn, a.d)
+                                 : ONESEG ? prv.tb + c * a.d : prv.tb + j + (8 * q + lr) * a.d;
+            *reinterpret_cast<float4*>(a.eout + ((size_t)prv.b * a.T + t) * C + cq) = fl4;
         }
     };
     // words and column times to LDS (all lanes write: identical values per column)
@@ -192,8 +215,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         }
     };
     auto epi2_max = [&]() {
-        const float m = wave_max(emax);
-        if (lane == 0) atomicMax(a.gmax_out + prv.b, __float_as_uint(m));
+        const uint32_t m = wave_max_bits(emax);
+        if (lane == 0) atomicMax(a.gmax_out + prv.b, m);
     };
 
     // ---- epilogue 1 of column half j, unit g in two parts: u, bits; v -> split v image ----
@@ -292,17 +315,21 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     if (blockIdx.x >= ntiles) return;   // (grid = min(tiles, CUs): not taken)
 
     // prologue: the first tile's image and residual rows; the second tile's rows in flight
+    float gm_c;     // max |e_l| of the current tile's clip (one scalar load per tile: the next one's)
     {
         const Tile t0 = tile_of(blockIdx.x);
 #pragma unroll
         for (int k = 0; k < NU; ++k) load_unit(t0, k);
         const uint32_t z0 = zero_bits_of(t0);
-        const float s0 = exp2i(scale_exp(sload(a.gmax_in + t0.b)));
+        gm_c = sload(a.gmax_in + t0.b);
+        const float s0 = exp2i(scale_exp(gm_c));
 #pragma unroll
         for (int k = 0; k < NU; ++k) conv_unit(k, &ER[0][0], s0, z0);
+#if !FWD_LOAD_AB
         const Tile t1 = tile_of(clampt(blockIdx.x + G));
 #pragma unroll
         for (int k = 0; k < NU; ++k) load_unit(t1, k);
+#endif
     }
 
     STAMP_DECL
@@ -317,27 +344,33 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         // T: the image of this tile complete (converted during the previous phase D)
         lds_barrier();
         STAMP(0)
-        const float gm = sload(a.gmax_in + cu.b);
+        const float gm = gm_c;
         const int m_e = scale_exp(gm);
         const int m_v = scale_exp(fmaf(a.wdn, gm, a.bdm));
-        const float s_next = exp2i(scale_exp(sload(a.gmax_in + nt.b)));
+        gm_c = sload(a.gmax_in + nt.b);
+        const float s_next = exp2i(scale_exp(gm_c));
         const uint32_t zn = zero_bits_of(nt);
         inv1 = exp2i(-(m_e + a.kd));
         sv = exp2i(m_v);
         uint8_t* erp = &ER[(it & 1) ^ 1][0];   // the previous tile's residual, then the next's
 
+        STAMP(10)
         // A: GEMM 1 half 0 + epilogue 2 of the previous tile
         if (!FIRST) {
             epi2_begin();
 #if defined(SW_EXP) && SW_EXP == 10
             gemm1h(J0{}, [&](int) {}, cu);
 #else
-            gemm1h(J0{}, [&](int st) { epi2_part(st / 3, st % 3, erp); }, cu);
+            gemm1h(J0{}, [&](int st) {
+                epi2_part(st / 3, st % 3, erp);
+                if (st >= 12 && st < 20) flush_part(0, (st - 12) >> 1, st & 1, erp);
+                if (FWD_LOAD_AB && st % 3 == 1 && st < 15) load_unit(nt, st / 3);
+            }, cu);
 #endif
             epi2_words();
             epi2_max();
         } else {
-            gemm1h(J0{}, [&](int) {}, cu);
+            gemm1h(J0{}, [&](int st) { if (FWD_LOAD_AB && st % 3 == 1 && st < 15) load_unit(nt, st / 3); }, cu);
         }
         STAMP(5)
         // B: GEMM 1 half 1 + epilogue 1 of half 0
@@ -346,7 +379,11 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
 #pragma unroll
         for (int st = 0; st < 8; ++st) epi1_part(0, st >> 1, st & 1);
 #else
-        gemm1h(J1{}, [&](int st) { if (st < 8) epi1_part(0, st >> 1, st & 1); }, cu);
+        gemm1h(J1{}, [&](int st) {
+            if (st < 8) epi1_part(0, st >> 1, st & 1);
+            else if (!FIRST && st < 16) flush_part(1, (st - 8) >> 1, st & 1, erp);
+            if (FWD_LOAD_AB && st >= 11 && st % 3 == 2) load_unit(nt, 5 + (st - 11) / 3);   // 11 14 17 20
+        }, cu);
 #endif
         lds_barrier();   // v image half 0, u > 0 words half 0, e > 0 words of tile i-1
         STAMP(1)
@@ -362,12 +399,12 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         gemm2h(J1{}, [&](int kb) {
             conv_unit(kb, erp, s_next, zn);
 #if !(defined(SW_EXP) && SW_EXP == 9)
-            load_unit(n2, kb);
+            if (!FWD_LOAD_AB) load_unit(n2, kb);
 #endif
             if (kb == 7) {
                 conv_unit(NU - 1, erp, s_next, zn);
 #if !(defined(SW_EXP) && SW_EXP == 9)
-                load_unit(n2, NU - 1);
+                if (!FWD_LOAD_AB) load_unit(n2, NU - 1);
 #endif
             }
         });
@@ -381,10 +418,15 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         tile_body(std::false_type{}, tile, it);
     // drain: epilogue 2 of the last tile
     {
-        const uint8_t* erl = &ER[(it - 1) & 1][0];
+        uint8_t* erl = &ER[(it - 1) & 1][0];
         epi2_begin();
 #pragma unroll
         for (int st = 0; st < 24; ++st) epi2_part(st / 3, st % 3, erl);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            flush_part(q >> 2, q & 3, 0, erl);
+            flush_part(q >> 2, q & 3, 1, erl);
+        }
         epi2_words();
         epi2_max();
         lds_barrier();

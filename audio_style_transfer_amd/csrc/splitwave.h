@@ -246,6 +246,20 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// max over the wave of non-negative floats (compared as their bits), uniform result: four DPP
+// steps make every row of 16 lanes uniform, then the four rows meet in scalar registers (the
+// __shfl_xor form is six dependent ds_bpermute round trips, ~500 exposed cycles per tile)
+__device__ __forceinline__ uint32_t wave_max_bits(float x) {
+    int v = __float_as_int(x);
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));   // row_half_mirror
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));   // row_mirror
+    const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return (uint32_t)max(max(a, b), max(c, d));
+}
+
 // [x > 0] as 0 / 1 for every non-NaN x: the bits as a signed integer clamped to [0, 1] (one
 // v_med3_i32; +0 and negatives give 0)
 __device__ __forceinline__ uint32_t pos_bit(float x) {
