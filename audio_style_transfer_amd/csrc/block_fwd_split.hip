@@ -7,20 +7,23 @@
 // One workgroup per CU (wave w owns output channels 32 w .. 32 w + 31), persistent over tiles
 // of 64 positions, one wave per SIMD: every epilogue runs in the shadow of MFMAs.  The two
 // 32-column halves j of a tile are separate MFMA phases, so the epilogue of one half overlaps
-// the GEMM of the other.  A tile's e_l arrives in registers a tile ahead, in rows (unit k:
-// image rows 8 k .. 8 k + 7 x wave w's 32 channels: 8 cache lines per wave instruction), and is
-// converted into the LDS image (split relu(e_l), scaled by 2^m_e from the clip's max |e_l|) and
-// into the wave's quarter of a residual buffer (fp32 e_l, double-buffered, read back by the
-// same wave only).  Per tile i:
+// the GEMM of the other.  A tile's e_l arrives in registers (rows: unit k = image rows 8 k ..
+// 8 k + 7 x wave w's 32 channels, 8 cache lines per wave instruction), loaded during phases A
+// and B of the previous tile, and is converted into the LDS image (split relu(e_l), scaled by
+// 2^m_e from the clip's max |e_l|) and into the wave's quarter of a residual buffer (fp32 e_l,
+// double-buffered, read back by the same wave only).  Per tile i:
 //   T  barrier (image i complete)
 //   A  GEMM 1, column half 0 (3 taps x 8 k-blocks x 3 products); carries epilogue 2 of tile
-//      i-1 (8 units of 3 steps: e_i = e_{i-1} + y + b_r -> HBM, e > 0 bits, max |e|)
+//      i-1 (8 units of 3 steps: e_i = e_{i-1} + y + b_r back into the residual rows, e > 0
+//      bits, max |e|), the flush of its half 0 (residual rows -> HBM as whole lines) and the
+//      row loads of tile i+1, units 0..4
 //   B  GEMM 1, column half 1; carries epilogue 1 of half 0 (u = acc 2^-(m_e+k_d) + b_d, u > 0
-//      bits, v = relu(u) 2^m_v -> split v image; m_v from the bound |u| <= wdn max|e_l| + bdm)
-//      barrier
+//      bits, v = relu(u) 2^m_v -> split v image; m_v from the bound |u| <= wdn max|e_l| + bdm),
+//      the flush of epilogue 2's half 1 and the row loads of units 5..8; barrier
 //   C  GEMM 2 (8 k-blocks x 3 products), half 0; carries epilogue 1 of half 1; barrier
-//   D  GEMM 2, half 1; carries the conversion of tile i+1 (image + residual) and, unit by
-//      unit behind it, the row loads of tile i+2
+//   D  GEMM 2, half 1; carries the conversion of tile i+1 (image + residual)
+// Round-2 measurements of this structure: ~13k cycles per tile against an MFMA
+// floor of 6.2k; moving the loads / conversions between phases does not change the tile time.
 #include "splitwave.h"
 #include <algorithm>
 #include <type_traits>
@@ -32,12 +35,6 @@ using namespace sw;
 constexpr int IROWS = 72;             // image / residual rows: 66 or 68 used, 9 units x 8 rows
 constexpr int ISLOT = IROWS * RS;     // bytes per image / residual buffer
 constexpr int LA = 2;                 // B-fragment lookahead (steps)
-#ifndef FWD_FLUSH
-#define FWD_FLUSH 1                   // epilogue 2 rows leave through LDS as whole lines (else direct)
-#endif
-#ifndef FWD_LOAD_AB
-#define FWD_LOAD_AB 1                 // next tile's row loads in phases A / B (else D, two tiles ahead)
-#endif
 
 template <bool MASKED, bool ONESEG>
 __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
@@ -179,11 +176,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             e2o.y = e2e.y + fmaf(acc2[j][4 * g + 1], inv2p, e2b.y);
             e2o.z = e2e.z + fmaf(acc2[j][4 * g + 2], inv2p, e2b.z);
             e2o.w = e2e.w + fmaf(acc2[j][4 * g + 3], inv2p, e2b.w);
-#if FWD_FLUSH
             *reinterpret_cast<float4*>(erp + Lc[j] * RS + 4 * (chb + 8 * g)) = e2o;
-#else
-            *reinterpret_cast<float4*>(a.eout + ((size_t)prv.b * a.T + ctime(prv, 32 * j + r, toff[j])) * C + chb + 8 * g) = e2o;
-#endif
         } else {
             emax = fmaxf(emax, fmaxf(fmaxf(fabsf(e2o.x), fabsf(e2o.y)), fmaxf(fabsf(e2o.z), fabsf(e2o.w))));
             // bit mbit(4 g + q) = 4 q + g of the column's word (common.h)
@@ -194,7 +187,6 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     // reads the row back, part 1 stores it
     float4 fl4;
     auto flush_part = [&](int j, int q, int part, const uint8_t* erp) {
-        if (!FWD_FLUSH) return;
         const int c = 32 * j + 8 * q + lr;
         if (part == 0) {
             const int row = (MASKED || ONESEG) ? c + 1 : 34 * j + 1 + 8 * q + lr;   // frow(c)
@@ -325,11 +317,6 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         const float s0 = exp2i(scale_exp(gm_c));
 #pragma unroll
         for (int k = 0; k < NU; ++k) conv_unit(k, &ER[0][0], s0, z0);
-#if !FWD_LOAD_AB
-        const Tile t1 = tile_of(clampt(blockIdx.x + G));
-#pragma unroll
-        for (int k = 0; k < NU; ++k) load_unit(t1, k);
-#endif
     }
 
     STAMP_DECL
@@ -340,8 +327,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         constexpr bool FIRST = decltype(first_tag)::value;
         const Tile cu = tile_of(tile);
         const Tile nt = tile_of(clampt(tile + G));
-        const Tile n2 = tile_of(clampt(tile + 2 * G));
-        // T: the image of this tile complete (converted during the previous phase D)
+                // T: the image of this tile complete (converted during the previous phase D)
         lds_barrier();
         STAMP(0)
         const float gm = gm_c;
@@ -364,13 +350,13 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             gemm1h(J0{}, [&](int st) {
                 epi2_part(st / 3, st % 3, erp);
                 if (st >= 12 && st < 20) flush_part(0, (st - 12) >> 1, st & 1, erp);
-                if (FWD_LOAD_AB && st % 3 == 1 && st < 15) load_unit(nt, st / 3);
+                if (st % 3 == 1 && st < 15) load_unit(nt, st / 3);   // rows of tile i+1: units 0..4
             }, cu);
 #endif
             epi2_words();
             epi2_max();
         } else {
-            gemm1h(J0{}, [&](int st) { if (FWD_LOAD_AB && st % 3 == 1 && st < 15) load_unit(nt, st / 3); }, cu);
+            gemm1h(J0{}, [&](int st) { if (st % 3 == 1 && st < 15) load_unit(nt, st / 3); }, cu);
         }
         STAMP(5)
         // B: GEMM 1 half 1 + epilogue 1 of half 0
@@ -382,14 +368,16 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         gemm1h(J1{}, [&](int st) {
             if (st < 8) epi1_part(0, st >> 1, st & 1);
             else if (!FIRST && st < 16) flush_part(1, (st - 8) >> 1, st & 1, erp);
-            if (FWD_LOAD_AB && st >= 11 && st % 3 == 2) load_unit(nt, 5 + (st - 11) / 3);   // 11 14 17 20
+            if (st >= 11 && st % 3 == 2) load_unit(nt, 5 + (st - 11) / 3);   // units 5..8: 11 14 17 20
         }, cu);
 #endif
         lds_barrier();   // v image half 0, u > 0 words half 0, e > 0 words of tile i-1
         STAMP(1)
         if (!FIRST) store_me(prv.b);
         // C: GEMM 2 half 0 + epilogue 1 of half 1
-        gemm2h(J0{}, [&](int kb) { epi1_part(1, kb >> 1, kb & 1); });
+        gemm2h(J0{}, [&](int kb) {
+            epi1_part(1, kb >> 1, kb & 1);
+        });
         lds_barrier();   // v image half 1, all u > 0 words
         STAMP(2)
         if (lane < 16)   // u > 0 words of the tile (this layer's positions): wave w, columns 16 w..
@@ -398,15 +386,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         // D: GEMM 2 half 1 + conversion of tile i+1, each unit's registers reloaded with i+2
         gemm2h(J1{}, [&](int kb) {
             conv_unit(kb, erp, s_next, zn);
-#if !(defined(SW_EXP) && SW_EXP == 9)
-            if (!FWD_LOAD_AB) load_unit(n2, kb);
-#endif
-            if (kb == 7) {
-                conv_unit(NU - 1, erp, s_next, zn);
-#if !(defined(SW_EXP) && SW_EXP == 9)
-                if (!FWD_LOAD_AB) load_unit(n2, NU - 1);
-#endif
-            }
+            if (kb == 7) conv_unit(NU - 1, erp, s_next, zn);
         });
         STAMP(3)
         prv = cu;

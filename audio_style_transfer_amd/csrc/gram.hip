@@ -29,12 +29,33 @@ __global__ void __launch_bounds__(256) k_style_ours(StyleArgs a) {
     for (int e = tid; e < LL; e += 256) EL[e] = (uint16_t)(((e / L) << 8) | (e % L));
     const int b = blockIdx.x / (C / 4);
     const int c = (blockIdx.x % (C / 4)) * 4 + w;
-    for (int e = lane; e < 1024; e += 64) {
-        float s = 0.f;
-        for (int ch = 0; ch < a.nchunk; ++ch)
-            s += a.gpart[(((size_t)b * a.nchunk + ch) * C + c) * 1024 + e];
-        Gu[w][(e >> 5) * 33 + (e & 31)] = s;
-        St[w][e] = 0.f;
+    // chunk partials: 16 independent loads in flight per lane (a serial chain of dependent
+    // load-add pairs ran at 1.6 TB/s); the sum order over chunks is fixed (ch ascending)
+    const float* gp = a.gpart + ((size_t)b * a.nchunk * C + c) * 1024;
+    const size_t cs = (size_t)C * 1024;
+    for (int e0 = 0; e0 < 1024; e0 += 256) {
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+        int ch = 0;
+        for (; ch + 4 <= a.nchunk; ch += 4) {
+            float v[4][4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[q][k] = gp[(ch + q) * cs + e0 + 64 * k + lane];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) s[k] += v[q][k];
+        }
+        for (; ch < a.nchunk; ++ch)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) s[k] += gp[ch * cs + e0 + 64 * k + lane];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int e = e0 + 64 * k + lane;
+            Gu[w][(e >> 5) * 33 + (e & 31)] = s[k];
+            St[w][e] = 0.f;
+        }
     }
     __syncthreads();
     // the list Gram is re-read from LDS wherever needed: per-lane copies of the <= 16
