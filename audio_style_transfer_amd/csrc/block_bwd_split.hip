@@ -287,7 +287,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             if (!FIRST && kb < 4) epi_part(1, (kb + 8) / 3, (kb + 8) % 3, ero, me_p, inv2p);
             gu_part(0, kb >> 1, kb & 1, f_u);
         });
-        if (!FIRST) epi_max(prv.b);
+        // max |out| of clip prv.b -> gmax_out once per run of tiles of one clip (omax runs on:
+        // with the clip-interleaved tile order a workgroup usually keeps its clip)
+        if (!FIRST && cu.b != prv.b) epi_max(prv.b);
         if (ONESEG) {
             // H: g_v of the halo columns + g_u of half 1; then g_u of the halo columns
             gemm1(J2{}, [&](int kb) { gu_part(1, kb >> 1, kb & 1, f_u); });
@@ -359,7 +361,7 @@ __global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, siz
 void launch_block_bwd_s(const BwdArgsS& a0, hipStream_t s) {
     BwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
-    a.ft = make_fdiv((uint32_t)(a.T / TMS));
+    a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));
     const int nt = a.B * (a.T / TMS);
     const dim3 grid(std::min(nt, sw::num_cus()));
     Layout ly;

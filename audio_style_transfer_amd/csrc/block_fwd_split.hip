@@ -162,8 +162,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     float emax = 0.f;
     uint32_t mb[2] = {0u, 0u};
     float4 e2e, e2b, e2o;
-    auto epi2_begin = [&]() {
-        emax = 0.f;
+    auto epi2_begin = [&]() {   // (emax runs on over the workgroup's consecutive tiles of one clip)
         mb[0] = mb[1] = 0u;
     };
     auto epi2_part = [&](int u, int part, uint8_t* erp) {
@@ -206,9 +205,12 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             MBT[c] = ctime(prv, c, toff[j]);
         }
     };
+    // max |e_{l+1}| of clip prv.b -> gmax_out, once per run of tiles of one clip (with the
+    // clip-interleaved tile order a workgroup usually keeps its clip for the whole launch)
     auto epi2_max = [&]() {
         const uint32_t m = wave_max_bits(emax);
         if (lane == 0) atomicMax(a.gmax_out + prv.b, m);
+        emax = 0.f;
     };
 
     // ---- epilogue 1 of column half j, unit g in two parts: u, bits; v -> split v image ----
@@ -354,7 +356,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             }, cu);
 #endif
             epi2_words();
-            epi2_max();
+            if (cu.b != prv.b) epi2_max();
         } else {
             gemm1h(J0{}, [&](int st) { if (st % 3 == 1 && st < 15) load_unit(nt, st / 3); }, cu);
         }
@@ -421,7 +423,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
 void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
     FwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
-    a.ft = make_fdiv((uint32_t)(a.T / TMS));
+    a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));
     const int nt = a.B * (a.T / TMS);
     const dim3 grid(std::min(nt, sw::num_cus()));
     Layout ly;

@@ -190,7 +190,7 @@ struct FwdArgsS {
     int dn_log2, nn;       // next layer: log2 dilation, T / dilation
     int kd, kr;            // weight exponents
     float wdn, bdm;        // max_co sum_{tap,ci} |W_d|, max |b_d|: |u| <= wdn max|e_l| + bdm
-    FDiv fn, ft;           // by n, by tiles per clip (T / 64): set by the launcher
+    FDiv fn, ft;           // by n; by B (or T / 64: splitwave.h tile order): set by the launcher
 };
 
 struct BwdArgsS {
@@ -206,7 +206,7 @@ struct BwdArgsS {
     int B, T, d, n;
     int kd, kr;
     float wrn;             // max_ci sum_co |W_r|: |W_r tot| <= wrn max|tot|
-    FDiv fn, ft;           // by n, by tiles per clip (T / 64): set by the launcher
+    FDiv fn, ft;           // by n; by B (or T / 64: splitwave.h tile order): set by the launcher
 };
 
 struct GramArgs {

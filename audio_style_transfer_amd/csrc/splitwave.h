@@ -69,11 +69,24 @@ __device__ __forceinline__ int row_toff(int L, const Layout& ly, int d) {
 
 struct Tile { int b, p0, tb, m0; };   // clip, first position, base time, p0 mod n
 
+// Tile order: clip-interleaved (SW_TILE_INTERLEAVE, ft divides by B): tile tl is clip tl mod B,
+// position block tl / B, so the workgroups of one round work on different clips and their
+// per-clip max atomics go to different words (clip-major order puts all 1024 waves' atomics of
+// a round on ONE word).  Otherwise clip-major (ft divides by T / 64).
+#ifndef SW_TILE_INTERLEAVE
+#define SW_TILE_INTERLEAVE 1
+#endif
 template <bool MASKED>
 __device__ __forceinline__ Tile tile_at(int tl, const FDiv& ft, const FDiv& fn, int d, const Layout& ly) {
     Tile t;
+#if SW_TILE_INTERLEAVE
+    const int pb = (int)fdiv((uint32_t)tl, ft);
+    t.b = tl - pb * (int)ft.n;
+    t.p0 = pb * TMS;
+#else
     t.b = (int)fdiv((uint32_t)tl, ft);
     t.p0 = (tl - t.b * (int)ft.n) * TMS;
+#endif
     const int q = (int)fdiv((uint32_t)t.p0, fn);
     t.m0 = t.p0 - q * (int)fn.n;
     t.tb = MASKED ? 0 : (ly.M == TMS ? t.m0 * d + q : q);
