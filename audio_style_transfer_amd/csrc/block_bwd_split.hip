@@ -50,6 +50,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
     const int G = (int)gridDim.x;
+    STAMP_DECL
 
     auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, a.ft, a.fn, a.d, ly); };
     auto clampt = [&](int tl) { return tl < ntiles ? tl : ntiles - 1; };
@@ -258,7 +259,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     }
 
     Tile prv = tile_of(blockIdx.x);
-    STAMP_DECL
+    STAMP(14)
     auto tile_body = [&](auto first_tag, int tile, int it) {
         constexpr bool FIRST = decltype(first_tag)::value;
         const Tile cu = tile_of(tile);

@@ -52,6 +52,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
     const int G = (int)gridDim.x;
+    STAMP_DECL
 
     auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, a.ft, a.fn, a.d, ly); };
     // tiles past the end repeat the last one (loaded and converted, never used)
@@ -321,7 +322,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         for (int k = 0; k < NU; ++k) conv_unit(k, &ER[0][0], s0, z0);
     }
 
-    STAMP_DECL
+    STAMP(13)
     // one tile; FIRST (the peeled first tile) has no pending epilogue 2.  Peeling keeps the
     // sequence of vector-memory operations identical in every loop iteration, so the compiler's
     // counted waits for the row loads never include the epilogue's stores.

@@ -34,18 +34,19 @@ if prec == 'bf16':
     tiles = B * T // 128 * 30 / 256   # tiles per CU over the 30 block launches
     groups = ((0, 4), (4, 8))
 else:
-    names = {0: 'fwd: T barrier', 10: 'fwd: top (scales, scalar loads)', 5: 'fwd: A GEMM1 half 0 + epi2(prev)',
+    names = {13: 'fwd: prologue (weights, first tile)', 14: 'bwd: prologue (weights, first tile)', 0: 'fwd: T barrier', 10: 'fwd: top (scales, scalar loads)', 5: 'fwd: A GEMM1 half 0 + epi2(prev)',
              1: 'fwd: B GEMM1 half 1 + epi1 half 0 + barrier', 2: 'fwd: C GEMM2 half 0 + epi1 half 1 + barrier',
              3: 'fwd: D GEMM2 half 1 + convert + loads', 4: 'fwd: drain',
              6: 'bwd: T barrier', 11: 'bwd: top (scales, scalar loads)', 7: 'bwd: A/B/H g_v + g_u + epi half 1 (prev) + barrier',
              8: 'bwd: C g_a half 0 + convert + loads', 9: 'bwd: D g_a half 1 + epi half 0',
              12: 'bwd: drain'}
     tiles = B * T // 64 * 30 / 256
-    for grp in ((0, 10, 5, 1, 2, 3, 4), (6, 11, 7, 8, 9, 12)):
+    for grp in ((13, 0, 10, 5, 1, 2, 3, 4), (14, 6, 11, 7, 8, 9, 12)):
         tot = sum(v[k] for k in grp)
         for k in grp:
             if v[k]:
                 print('%-48s %6.1f %%   %8.0f cycles/tile/wave' % (names[k], 100.0 * v[k] / tot, v[k] / (4 * 256 * tiles)))
+        print('%-48s %8.0f cycles per wave per launch' % ('total', tot / (4 * 256 * 30)))
     sys.exit(0)
 for lo, hi in groups:
     tot = sum(v[lo:hi])
