@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         const int m_u = scale_exp(a.wrn * gm);
         const float f_u = exp2i(m_u - m_t - a.kr);   // acc units 2^(m_t + k_r) -> g_u 2^m_u
         const float inv2 = exp2i(-(m_u + a.kd));
-        gm_c = sload(a.gmax_in + nt.b);
+        if (nt.b != cu.b) gm_c = sload(a.gmax_in + nt.b);   // (usually the same clip: tile order)
         const float s_next = exp2i(scale_exp(gm_c));
         const uint32_t zn = ru.zero_bits(nt, a.fn);
         uint8_t* erc = &ER[it & 1][0];          // this tile's residual

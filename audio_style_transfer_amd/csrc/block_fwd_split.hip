@@ -336,7 +336,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         const float gm = gm_c;
         const int m_e = scale_exp(gm);
         const int m_v = scale_exp(fmaf(a.wdn, gm, a.bdm));
-        gm_c = sload(a.gmax_in + nt.b);
+        if (nt.b != cu.b) gm_c = sload(a.gmax_in + nt.b);   // (usually the same clip: tile order)
         const float s_next = exp2i(scale_exp(gm_c));
         const uint32_t zn = zero_bits_of(nt);
         inv1 = exp2i(-(m_e + a.kd));

@@ -246,8 +246,12 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
         bk[j] = b0[m * 8 + j];
     }
     float amax = 0.f;
+    // clip-interleaved block order (block i: clip i mod B, row chunk i / B): concurrently running
+    // workgroups belong to different clips, so their max atomics do not pile onto one word
+    const int nper = T / SFR;
+    const size_t lb = (size_t)(blockIdx.x % B) * nper + blockIdx.x / B;
     for (int it = 0; it < SFR / 16; ++it) {
-        const size_t rowi = (size_t)blockIdx.x * SFR + it * 16 + (threadIdx.x >> 4);
+        const size_t rowi = lb * SFR + it * 16 + (threadIdx.x >> 4);
         const int t = (int)(rowi % T);
         const float* xr = x + (rowi - t);
         const float xm = t > 0 ? xr[t - 1] / 128.0f : 0.f;
@@ -308,7 +312,7 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
         // max |e_0| of the workgroup's rows (one clip: T is a multiple of SFR) -> the clip's max
         amax = wave_max_f(amax);
         if ((threadIdx.x & 63) == 0)
-            atomicMax(gmax + (size_t)blockIdx.x * SFR / T, __float_as_uint(amax));
+            atomicMax(gmax + blockIdx.x % B, __float_as_uint(amax));
     }
 }
 
