@@ -201,21 +201,25 @@ def run(args, Eng, precision, steps, warmup, ws, rank, dev, graph, clips=None, g
     return el, tm, first_loss, last_loss, bad
 
 
-def grad_check(Eng, precision, dev):
+def grad_check(Eng, precision, dev, gatys=False):
     """d loss / d x of one 2048-sample clip against the committed fp64 oracle gradient
-    (tests/golden: 'ours' = 30 style layers, content layer 25, the oracle's own targets)."""
+    (tests/golden: 'ours' = 30 style layers, content layer 25; 'gatys' (--gatys) = 30 Gatys
+    style layers, content layer 29; the oracle's own targets, stored in fp32)."""
     import torch
+    tag = 'gatys' if gatys else 'ours'
     g = np.load(os.path.join(ROOT, 'tests', 'golden', 'oracle_T2048.npz'))
     tg = np.load(os.path.join(ROOT, 'tests', 'golden', 'oracle_T2048_targets.npz'))
-    eng = Eng(1, 2048, [25], list(range(30)), precision=precision, device=dev, lambd=100.0)
-    eng.set_targets(torch.tensor(tg['ours_phi_c']), torch.tensor(tg['ours_phi_s']))
-    parts, grad = eng.loss_grad(torch.tensor(g['ours_x'][None], dtype=torch.float32, device=dev))
+    eng = Eng(1, 2048, [29] if gatys else [25], list(range(30)), precision=precision, device=dev,
+              lambd=100.0, gatys=gatys)
+    eng.set_targets(torch.tensor(tg[tag + '_phi_c']), torch.tensor(tg[tag + '_phi_s']))
+    parts, grad = eng.loss_grad(torch.tensor(g[tag + '_x'][None], dtype=torch.float32, device=dev))
     grad = grad.cpu().double().numpy()[0]
     loss = float(parts[0, 0])
     eng.close()
-    ref = g['ours_grad']
-    return {'grad_rel_l2': float(np.linalg.norm(grad - ref) / np.linalg.norm(ref)),
-            'loss_rel': abs(loss - float(g['ours_parts'][0])) / abs(float(g['ours_parts'][0]))}
+    ref = g[tag + '_grad']
+    return {'grad_check_case': tag,
+            'grad_rel_l2': float(np.linalg.norm(grad - ref) / np.linalg.norm(ref)),
+            'loss_rel': abs(loss - float(g[tag + '_parts'][0])) / abs(float(g[tag + '_parts'][0]))}
 
 
 def cpu_baseline(T, budget_s, gatys=False):
@@ -318,7 +322,7 @@ def rank_main(args):
                                  'kernels_ms_per_step': {k[:-3]: tm2[k] / calls for k in
                                                          ('block_fwd_ms', 'block_bwd_ms',
                                                           'gram_fwd_ms', 'gram_bwd_ms', 'other_ms')},
-                                 **grad_check(Eng, p, dev)}
+                                 **grad_check(Eng, p, dev, args.gatys)}
         for p in ('split', 'fp32'):     # configs[1]: one 16384-sample clip
             e1, _, _, _, _ = run(args, Eng, p, 10 * args.side_steps, 2, ws, rank, dev,
                                  bool(args.graph), clips=1, gatys=False)
@@ -371,7 +375,7 @@ def rank_main(args):
         'nonfinite_clips': bad,
     }
     if dev.type == 'cuda':
-        out.update(grad_check(Eng, args.precision, dev))
+        out.update(grad_check(Eng, args.precision, dev, args.gatys))
     out.update(side)
     if ws == 1 and args.cpu_baseline_seconds > 0:
         out['cpu_baseline'] = cpu_baseline(T, args.cpu_baseline_seconds, args.gatys)

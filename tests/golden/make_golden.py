@@ -126,7 +126,7 @@ def oracle_vectors():
     from audio_style_transfer_amd.weights import synthetic_weights, synthetic_clips
     W = synthetic_weights(0)
     T = 2048
-    out = {}
+    out, tgt = {}, {}
     for tag, kw in [('ours', dict(cont_ids=[25], style_ids=list(range(30)), gatys=False,
                                   nb_channels=128, cnt_channels=128)),
                     ('c1', dict(cont_ids=[25], style_ids=list(range(10)), gatys=False,
@@ -141,13 +141,14 @@ def oracle_vectors():
         rng = np.random.default_rng(7)
         x = (O.mu_law_numpy(synthetic_clips(1, T, 42)[0]) + rng.normal(0, 4, T))
         parts, g = O.loss_and_grad(x, W, phi_c=phi_c, phi_s=phi_s, lambd=100.0, gamma=0.0, **kw)
-        if tag == 'ours':   # targets for bench.py's per-precision gradient check
-            np.savez_compressed(os.path.join(HERE, 'oracle_T2048_targets.npz'),
-                                ours_phi_c=phi_c.astype(np.float32), ours_phi_s=phi_s.astype(np.float32))
+        if tag in ('ours', 'gatys'):   # targets for bench.py's per-precision gradient check
+            tgt[tag + '_phi_c'] = phi_c.astype(np.float32)
+            tgt[tag + '_phi_s'] = phi_s.astype(np.float32)
         out[tag + '_x'] = x
         out[tag + '_parts'] = parts
         out[tag + '_grad'] = g
     np.savez_compressed(os.path.join(HERE, 'oracle_T2048.npz'), **out)
+    np.savez_compressed(os.path.join(HERE, 'oracle_T2048_targets.npz'), **tgt)
 
 
 if __name__ == '__main__':
