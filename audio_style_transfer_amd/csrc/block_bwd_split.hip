@@ -19,8 +19,10 @@
 //      i-1 (out = residual + [e_l > 0] g_a 2^-(m_u+k_d) -> HBM)
 //   B  g_v column half 1; carries the rest of that epilogue and g_u of half 0 (mask, scale
 //      2^m_u from the bound |g_v| <= wrn max|tot|, split -> g_u image)
-//   H  (one-segment layouts) g_v of the two halo columns; carries g_u of half 1
-//      g_u of the last column tile; barrier (g_u image complete, tot image free)
+//   H  (one-segment layouts, unless the workgroup's previous tile is the left neighbour: then
+//      its g_u rows 64 / 65 are copied to rows 0 / 1) g_v of rows 0 / 1 (positions p0 - 1, p0;
+//      the column tiles cover p0 + 1 .. p0 + 64); carries g_u of half 1; g_u of the last column
+//      tile; barrier (g_u image complete, tot image free)
 //   C  g_a, column half 0 (3 taps x 8 k-steps x 3 products over the g_u image); carries the
 //      conversion of tile i+1 and, unit by unit behind it, the row loads of tile i+2
 //   D  g_a, column half 1; carries epilogue half 0 of tile i
@@ -81,9 +83,16 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     }
     const int chb = 32 * w + 4 * h;
     auto ctime = [&](const Tile& t, int cc, int to) { return col_time<MASKED>(t, cc, to, a.fn, a.d); };
-    // the halo column tile (one-segment layouts): lane r == 0 -> image row 0 (p0 - 1), r == 1 ->
-    // row 65 (p0 + 64); lanes r >= 2 compute a copy of row 0 and write it to unused row 66
-    const int Lh = r == 1 ? TMS + 1 : 0;
+    // g_v / g_u rows.  One-segment layouts shift the two column tiles by one row: they cover
+    // image rows 2..65 (positions p0 + 1 .. p0 + 64, the right halo included), and rows 0 / 1
+    // (p0 - 1, p0) are either the previous tile's rows 64 / 65 (the workgroup's previous tile is
+    // the left neighbour in the same sub-sequence: copied, no MFMAs) or the halo tile's
+    // (lane r == 0 -> row 0, r == 1 -> row 1; lanes r >= 2 compute a copy of row 0 and write it
+    // to unused row 66).  Other layouts: the tile's columns, no halo rows.
+    int Lv[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) Lv[j] = ONESEG ? Lc[j] + 1 : Lc[j];
+    const int Lh = r == 1 ? 1 : 0;
     const int Lhw = r < 2 ? Lh : TMS + 2;
 
     // ---- rows of the next tile: tot (-> split image) and D_l (-> residual) ----
@@ -113,13 +122,15 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         const size_t cb = (size_t)t.b * a.T + t.p0;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            mu[j] = a.mu[(cb + 32 * j + r) * 8 + 4 * h + w];
+            // u > 0 of the g_v rows Lv[j]; a position past the clip reads any word (its tot row
+            // is zero)
+            const int pv = ONESEG ? min(t.p0 + 1 + 32 * j + r, a.T - 1) : t.p0 + 32 * j + r;
+            mu[j] = a.mu[((size_t)t.b * a.T + pv) * 8 + 4 * h + w];
             me[j] = a.me[(cb + 32 * j + r) * 8 + 4 * h + w];
         }
-        if (ONESEG) {   // a halo outside the clip reads any word: its tot row is zero
-            int p = t.p0 + (r == 1 ? TMS : -1);
-            p = p < 0 ? 0 : (p >= a.T ? a.T - 1 : p);
-            muh = a.mu[((size_t)t.b * a.T + p) * 8 + 4 * h + w];
+        if (ONESEG) {   // rows 0 / 1: p0 - 1 (outside the clip at p0 == 0: its tot row is zero), p0
+            const int p = t.p0 + (r == 1 ? 0 : -1);
+            muh = a.mu[((size_t)t.b * a.T + (p < 0 ? 0 : p)) * 8 + 4 * h + w];
         }
     };
 
@@ -127,7 +138,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     f32x16 acc1[3];
     auto gemm1 = [&](auto j_tag, auto side) {
         constexpr int J = decltype(j_tag)::value;
-        const int row = J < 2 ? Lc[J] : Lh;
+        const int row = J < 2 ? Lv[J] : Lh;
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc1[J][i] = 0.f;
         uint4 bh[LA + 1], bl[LA + 1];
@@ -163,7 +174,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             // split's low half fuses with it into one v_fma_mix_f32
             uint2 hi, lo;
             split4(gq.x * f, gq.y * f, gq.z * f, gq.w * f, hi, lo);
-            uint8_t* p = XG + (J < 2 ? Lc[J] : Lhw) * RS + 2 * (chb + 8 * g);
+            uint8_t* p = XG + (J < 2 ? Lv[J] : Lhw) * RS + 2 * (chb + 8 * g);
             *reinterpret_cast<uint2*>(p) = hi;
             *reinterpret_cast<uint2*>(p + 256) = lo;
         }
@@ -279,6 +290,15 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         uint8_t* erc = &ER[it & 1][0];          // this tile's residual
         uint8_t* ero = &ER[(it & 1) ^ 1][0];    // the previous tile's, then the next tile's
 
+        // rows 0 / 1 from the previous tile's rows 64 / 65 when it is the left neighbour (every
+        // wave its channel quarter; the previous tile's g_a reads are behind the T barrier, this
+        // tile's first writes to rows 64 / 65 come in B)
+        const bool cont = ONESEG && !FIRST && prv.b == cu.b && prv.p0 + TMS == cu.p0 && cu.m0 != 0;
+        if (cont && lane < 16) {
+            const int o = ((lane >> 2) & 1) * 256 + 64 * w + 16 * (lane & 3);
+            const uint4 v = lds16(XG + (TMS + (lane >> 3)) * RS + o);
+            *reinterpret_cast<uint4*>(XG + (lane >> 3) * RS + o) = v;
+        }
         STAMP(11)
         // A: g_v half 0 + epilogue half 1 of the previous tile (parts 0..7)
         if (!FIRST) epi_begin(prv, 1);
@@ -291,8 +311,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         // max |out| of clip prv.b -> gmax_out once per run of tiles of one clip (omax runs on:
         // with the clip-interleaved tile order a workgroup usually keeps its clip)
         if (!FIRST && cu.b != prv.b) epi_max(prv.b);
-        if (ONESEG) {
-            // H: g_v of the halo columns + g_u of half 1; then g_u of the halo columns
+        if (ONESEG && !cont) {
+            // H: g_v of rows 0 / 1 + g_u of half 1; then g_u of rows 0 / 1
             gemm1(J2{}, [&](int kb) { gu_part(1, kb >> 1, kb & 1, f_u); });
 #pragma unroll
             for (int q = 0; q < 8; ++q) gu_part(2, q >> 1, q & 1, f_u);
