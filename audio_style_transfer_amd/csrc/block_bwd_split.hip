@@ -294,15 +294,18 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         // wave its channel quarter; the previous tile's g_a reads are behind the T barrier, this
         // tile's first writes to rows 64 / 65 come in B)
         const bool cont = ONESEG && !FIRST && prv.b == cu.b && prv.p0 + TMS == cu.p0 && cu.m0 != 0;
-        if (cont && lane < 16) {
-            const int o = ((lane >> 2) & 1) * 256 + 64 * w + 16 * (lane & 3);
-            const uint4 v = lds16(XG + (TMS + (lane >> 3)) * RS + o);
-            *reinterpret_cast<uint4*>(XG + (lane >> 3) * RS + o) = v;
-        }
+        const int cpo = ((lane >> 2) & 1) * 256 + 64 * w + 16 * (lane & 3);   // (side work of A)
+        uint4 cpv = make_uint4(0, 0, 0, 0);
         STAMP(11)
         // A: g_v half 0 + epilogue half 1 of the previous tile (parts 0..7)
         if (!FIRST) epi_begin(prv, 1);
-        gemm1(J0{}, [&](int kb) { if (!FIRST) epi_part(1, kb / 3, kb % 3, ero, me_p, inv2p); });
+        gemm1(J0{}, [&](int kb) {
+            if (!FIRST) epi_part(1, kb / 3, kb % 3, ero, me_p, inv2p);
+            if (cont && lane < 16) {   // rows 64 / 65 -> 0 / 1, read one step before the write
+                if (kb == 0) cpv = lds16(XG + (TMS + (lane >> 3)) * RS + cpo);
+                if (kb == 1) *reinterpret_cast<uint4*>(XG + (lane >> 3) * RS + cpo) = cpv;
+            }
+        });
         // B: g_v half 1 + the epilogue's parts 8..11 + g_u of half 0
         gemm1(J1{}, [&](int kb) {
             if (!FIRST && kb < 4) epi_part(1, (kb + 8) / 3, (kb + 8) % 3, ero, me_p, inv2p);
@@ -326,13 +329,16 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         //    right away (a tile of latency before the next conversion: issued later, the loads'
         //    latency shows)
         gemm2(J0{}, [&](int st) {
-            if (st < NU) {
-                conv_unit(st, ero, s_next, zn);
+            // unit k at step 24 k / 9 (0 2 5 8 10 13 16 18 21): spread over the phase
+#pragma unroll
+            for (int k = 0; k < NU; ++k)
+                if (st == (24 * k) / NU) {
+                    conv_unit(k, ero, s_next, zn);
 #if !(defined(SW_EXP) && SW_EXP == 9)
-                load_unit(n2, st);
+                    load_unit(n2, k);
 #endif
-            }
-            if (st == NU) load_masks(nt, mu_n, muh_n, me_n);
+                }
+            if (st == 3) load_masks(nt, mu_n, muh_n, me_n);
         }, cu);
         STAMP(8)
         // D: g_a half 1 + epilogue half 0 of this tile
