@@ -246,13 +246,10 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
 }
 
 // ---- fp32 mode (precision 0): the same staging and data movement on fp32 MFMA ----
-// forward: image [c][u][t] fp32 (row stride FRF floats: 80 B, conflict-free reads); lane (r, h)
-// reads E_r[t0 + 8 h .. + 8][c] (two 16-B reads) and runs 8 v_mfma_f32_32x32x2f32 with A = B
-// = that value (k-step s takes time 8 h + s: any common permutation of K is the same Gram).
+// forward: image [c][u][t] fp32 (row stride FRF floats: 80 B, conflict-free 16-B reads); the
+// symmetric Gram as three v_mfma_f32_16x16x4f32 tiles (U0 U0, U0 U1, U1 U1; U = 16 tensors) per
+// k-step, the fourth written as the mirror of (U0, U1): 3/4 of the MFMA cycles of one 32x32 tile.
 constexpr int FRF = 20;
-__device__ __forceinline__ f32x16 mfma_f32_32(float a, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, a, c, 0, 0, 0);
-}
 
 __global__ void __launch_bounds__(GWT) k_gram_fwd_f(GramArgs a) {
     __shared__ __attribute__((aligned(16))) float I[GCS * 32 * FRF];   // [c][u][t]
@@ -260,18 +257,18 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_f(GramArgs a) {
     decode(a, b, ch, c0);
     const int tlen = a.T / a.nchunk, tbeg = ch * tlen;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r = lane & 31, h = lane >> 5;
+    const int i16 = lane & 15, kq = lane >> 4;
     const int su = 8 * (w & 3) + (lane & 7), sq = lane >> 3, tb = w >> 2;
     const bool real = su < a.nu;
     const float* src = real ? (const float*)a.act + (size_t)a.uid[su] * a.tstride +
                               (size_t)b * a.T * C + c0 + 4 * sq + (size_t)8 * tb * C
                             : (const float*)a.zero16;
     const size_t rs = real ? C : 0;
-    f32x16 acc[4];
+    f32x4 acc[4][3];   // per channel: Gram tiles (U0, U0), (U0, U1), (U1, U1); (U1, U0) = mirror
 #pragma unroll
     for (int cc = 0; cc < 4; ++cc)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[cc][i] = 0.f;
+        for (int q = 0; q < 3; ++q) acc[cc][q] = f32x4{0.f, 0.f, 0.f, 0.f};
     float4 v0[8], v1[8];
     auto load = [&](float4 (&v)[8], int t0) {
 #pragma unroll
@@ -294,19 +291,20 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_f(GramArgs a) {
             *reinterpret_cast<float4*>(row + 4) = f[j][1];
         }
         __syncthreads();
+        // 16x16x4 tiles: lane (i16, kq) supplies tensor U + i16 at rows 4 kq .. 4 kq + 3 (k-step s
+        // takes row 4 kq + s: any common permutation of K is the same Gram) for A and B alike
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc) {
-            const float* row = &I[((4 * w + cc) * 32 + r) * FRF + 8 * h];
-            const float4 p = *reinterpret_cast<const float4*>(row);
-            const float4 q = *reinterpret_cast<const float4*>(row + 4);
-            acc[cc] = mfma_f32_32(p.x, acc[cc]);
-            acc[cc] = mfma_f32_32(p.y, acc[cc]);
-            acc[cc] = mfma_f32_32(p.z, acc[cc]);
-            acc[cc] = mfma_f32_32(p.w, acc[cc]);
-            acc[cc] = mfma_f32_32(q.x, acc[cc]);
-            acc[cc] = mfma_f32_32(q.y, acc[cc]);
-            acc[cc] = mfma_f32_32(q.z, acc[cc]);
-            acc[cc] = mfma_f32_32(q.w, acc[cc]);
+            const float* base = &I[(4 * w + cc) * 32 * FRF + 4 * kq];
+            const float4 u0 = *reinterpret_cast<const float4*>(base + i16 * FRF);
+            const float4 u1 = *reinterpret_cast<const float4*>(base + (16 + i16) * FRF);
+            const float a0[4] = {u0.x, u0.y, u0.z, u0.w}, a1[4] = {u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                acc[cc][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[st], a0[st], acc[cc][0], 0, 0, 0);
+                acc[cc][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[st], a1[st], acc[cc][1], 0, 0, 0);
+                acc[cc][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[st], a1[st], acc[cc][2], 0, 0, 0);
+            }
         }
     };
     load(v0, tbeg);
@@ -316,10 +314,16 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_f(GramArgs a) {
         stage(v1, t0 + GSS);
     }
 #pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
+    for (int cc = 0; cc < 4; ++cc) {   // lane holds G[U + 4 kq + i][U' + i16] (C/D map of 16x16x4)
         float* dst = a.gpart + (((size_t)b * a.nchunk + ch) * C + c0 + 4 * w + cc) * 1024;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) dst[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = acc[cc][i];
+        for (int i = 0; i < 4; ++i) {
+            const int rr = 4 * kq + i;
+            dst[rr * 32 + i16] = acc[cc][0][i];
+            dst[rr * 32 + 16 + i16] = acc[cc][1][i];
+            dst[(16 + i16) * 32 + rr] = acc[cc][1][i];
+            dst[(16 + rr) * 32 + 16 + i16] = acc[cc][2][i];
+        }
     }
 }
 
