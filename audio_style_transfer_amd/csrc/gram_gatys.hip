@@ -188,7 +188,8 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_bf16(GatysArgs a) {
         *reinterpret_cast<uint4*>(&Sb[row * SBS + c16 * 8]) =
             *reinterpret_cast<const uint4*>(S + row * C + c16 * 8);
     }
-    u16* E = (u16*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;
+    const u16* E = (const u16*)a.act + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;
+    u16* Ew = (u16*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;   // D (in place unless out of place)
     const u16* CG = (const u16*)a.cg[u];
     if (CG) CG += (size_t)b * a.T * C;
     const int j = lane & 31, kg = lane >> 5;
@@ -217,7 +218,7 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_bf16(GatysArgs a) {
                 acc[m] = mfma_bf16(*reinterpret_cast<const uint4*>(Ab + 32 * m * SBS + 8 * s),
                                    bcur[s], acc[m]);
         // lane holds time t + j, channels 32m + 8g + 4kg + 0..3 in acc[m][4g..4g+3]
-        u16* out = E + (size_t)(t + j) * C + 4 * kg;
+        u16* out = Ew + (size_t)(t + j) * C + 4 * kg;
         const u16* cgr = CG ? CG + (size_t)(t + j) * C + 4 * kg : nullptr;
 #pragma unroll
         for (int m = 0; m < 4; ++m)
@@ -249,7 +250,8 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_f32(GatysArgs a) {
     const float* S = a.smat + ((size_t)b * a.nu + u) * (C * C);
     for (int i = tid; i < C * C; i += 256) Sf[(i >> 7) * SFS + (i & 127)] = S[i];
     __syncthreads();
-    float* E = (float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;
+    const float* E = (const float*)a.act + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;
+    float* Ew = (float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;   // D (in place unless out of place)
     const float* CG = (const float*)a.cg[u];
     if (CG) CG += (size_t)b * a.T * C;
     const int j = lane & 31, kg = lane >> 5;
@@ -273,7 +275,7 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_f32(GatysArgs a) {
         for (int s = 0; s < 64; ++s)
 #pragma unroll
             for (int m = 0; m < 4; ++m) acc[m] = mfma_f32(Ab[32 * m * SFS + s], bf[s], acc[m]);
-        float* out = E + (size_t)(t + j) * C + 4 * kg;
+        float* out = Ew + (size_t)(t + j) * C + 4 * kg;
         const float* cgr = CG ? CG + (size_t)(t + j) * C + 4 * kg : nullptr;
 #pragma unroll
         for (int m = 0; m < 4; ++m)
@@ -402,7 +404,8 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s(GatysArgs a) {
         *reinterpret_cast<uint4*>(&Sh[row * SBS + c8 * 8]) = make_uint4(h[0], h[1], h[2], h[3]);
         *reinterpret_cast<uint4*>(&Sl[row * SBS + c8 * 8]) = make_uint4(l[0], l[1], l[2], l[3]);
     }
-    float* E = (float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;
+    const float* E = (const float*)a.act + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;
+    float* Ew = (float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;   // D (in place unless out of place)
     const float* CG = (const float*)a.cg[u];
     if (CG) CG += (size_t)b * a.T * C;
     const int j = lane & 31, kg = lane >> 5;
@@ -444,7 +447,7 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s(GatysArgs a) {
             }
         }
         // lane holds time t + j, channels 32m + 8g + 4kg + 0..3 in acc[m][4g..4g+3]
-        float* out = E + (size_t)(t + j) * C + 4 * kg;
+        float* out = Ew + (size_t)(t + j) * C + 4 * kg;
         const float* cgr = CG ? CG + (size_t)(t + j) * C + 4 * kg : nullptr;
 #pragma unroll
         for (int m = 0; m < 4; ++m)
