@@ -352,6 +352,7 @@ GramArgs gram_args(ast_ctx* x) {
     for (int u = 0; u < x->nu; ++u) { g.uid[u] = x->uid[u]; g.cg[u] = x->cg_buf[x->uid[u]]; }
     g.gpart = x->gpart; g.smat = x->smat; g.zero16 = x->zero;
     g.B = x->cfg.batch; g.T = x->cfg.T; g.nchunk = x->nchunk;
+    g.top_u = -1; g.gmax_top = nullptr;
     return g;
 }
 
@@ -783,6 +784,7 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     }
     // style (methods.py:62-76, 118-119)
     tmark(x, s);
+    bool top_max_done = false;   // split: the Gram bwd recorded the top tensor's per-clip max
     if (c.gatys) {
         GatysArgs g = gatys_args(x);
         launch_gatys_fwd(g, x->split ? 2 : (x->bf ? 1 : 0), s);
@@ -804,6 +806,12 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
         sa.smat = x->smat; sa.spart = x->spart;
         launch_style_ours(sa, s);
         tmark(x, s);
+        if (x->split && x->tensor_in_style[x->nblk]) {   // the chain's first max |tot| inside the Gram bwd
+            for (int u = 0; u < x->nu; ++u) if (x->uid[u] == x->nblk) g.top_u = u;
+            g.gmax_top = x->gmax_g + (size_t)x->nblk * c.batch;
+            HIPCHK(hipMemsetAsync(x->gmax_g, 0, (size_t)(NBLK_MAX + 1) * c.batch * 4, s));
+            top_max_done = g.top_u >= 0;
+        }
         launch_gram_bwd_any(x, g, s);
     }
     tmark(x, s);
@@ -811,7 +819,7 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     auto direct = [&](int t) -> const void* {   // D_t: direct loss gradient of tensor t (or null)
         return x->tensor_in_style[t] ? (x->dgrad ? (const void*)((char*)x->dgrad + (size_t)t * x->tstride * x->esz) : tens(x, t)) : x->cg_buf[t];
     };
-    if (x->split) {
+    if (x->split && !top_max_done) {
         HIPCHK(hipMemsetAsync(x->gmax_g, 0, (size_t)(NBLK_MAX + 1) * c.batch * 4, s));
         const void* top = direct(x->nblk);
         if (!top) return fail(AST_E_STATE, "top block has no loss gradient");

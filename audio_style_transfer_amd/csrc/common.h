@@ -218,6 +218,8 @@ struct GramArgs {
     const float* smat;                      // [B][C][32][32]
     const void* zero16;                     // >= 16 zero bytes
     int B, T, nchunk;
+    int top_u;                              // split bwd: unique tensor whose per-clip max |D| ...
+    unsigned* gmax_top;                     // ... goes to gmax_top[b] (atomic max of float bits), or -1
 };
 
 struct StyleArgs {

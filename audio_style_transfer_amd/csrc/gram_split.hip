@@ -140,6 +140,7 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     const int tlen = a.T / a.nchunk, tbeg = ch * tlen, tend = tbeg + tlen;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    float omax = 0.f;   // max |D| of tensor top_u (the backward chain's first input: no k_absmax pass)
     const int i16 = lane & 15, kq = lane >> 4;
     // A fragments (16x16x32): S~_c[u = 16 m + i16][u' = 8 kq .. + 8] as bf16 hi / lo; wave w
     // owns channels 4 w .. 4 w + 3
@@ -233,6 +234,8 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
                         o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
                     }
                     *reinterpret_cast<float4*>((float*)a.actw + off) = o;
+                    if (u == a.top_u)
+                        omax = fmaxf(omax, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
                 }
             }
         }
@@ -242,6 +245,19 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     for (int t0 = tbeg; t0 < tend; t0 += 2 * GSS) {
         stage(v0, t0);
         stage(v1, t0 + GSS);
+    }
+    if (a.top_u >= 0) {   // one atomic per workgroup
+        __shared__ float wm[GWT / 64];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) omax = fmaxf(omax, __shfl_xor(omax, off));
+        if (lane == 0) wm[w] = omax;
+        __syncthreads();
+        if (tid == 0) {
+            float m = wm[0];
+#pragma unroll
+            for (int k = 1; k < GWT / 64; ++k) m = fmaxf(m, wm[k]);
+            atomicMax(a.gmax_top + b, __float_as_uint(m));
+        }
     }
 }
 
