@@ -126,8 +126,9 @@ struct ast_ctx {
     float2* stft_tw = nullptr;              // STFT regulariser: twiddles [1024]
     float* stft_fpart = nullptr;            //   per-frame partial sums [B][nf]
     float* stft_gfr = nullptr;              //   per-frame gradients [B][nf][1024]
-    bool lb_begun = false;                  // some workspace was started (ast_lbfgs_begin)
+    std::vector<const void*> lb_ws;         // workspaces started here with x0 (ast_lbfgs_begin)
     void* zero = nullptr;                   // 256 zero bytes
+    int* rflags = nullptr;                  // [B] AST_RANGE_* of the last ast_loss_grad
     size_t gpart_elems = 0, smat_elems = 0; // per context (mode-dependent)
     int ncpart = 0;
     std::vector<void*> allocs;
@@ -145,6 +146,17 @@ struct ast_ctx {
 namespace {
 
 int ext_to_tensor(int ext) { return ext >= 30 ? 30 : ext + 1; }
+
+// Number of Gram time chunks of a T-sample clip: every chunk a whole number of the kernels'
+// `stage`-row stages (the kernels loop stage by stage up to the chunk end), as many chunks as
+// divide evenly up to T / `target` (about `target` rows each).  T = 16384: 16 (ours), 4 (Gatys);
+// T = 3584: 2 x 1792 rows (T / 1024 = 3 does not divide the 112 stages).
+int gram_chunks(int T, int stage, int target) {
+    const int stages = T / stage;                     // T is a multiple of 512
+    int n = std::max(1, std::min(stages, T / target));
+    while (stages % n) --n;
+    return n;
+}
 
 int plan(const ast_cfg* c, ast_ctx* x) {
     if (c->batch < 1 || c->T < 512 || c->T % 512)
@@ -194,11 +206,11 @@ int plan(const ast_cfg* c, ast_ctx* x) {
     // so its result, bit for bit) do not depend on how many clips share the context
     int nch = 1;
     if (c->gatys) {
-        nch = std::max(1, c->T / 4096);        // multiples of 64 rows
+        nch = gram_chunks(c->T, 64, 4096);     // whole 64-row stages (bf16 / split; fp32: 32)
         x->gpart_elems = (size_t)c->batch * nch * x->nu * C * C;
         x->smat_elems = (size_t)c->batch * x->nu * C * C;
     } else {
-        nch = std::max(1, c->T / 1024);        // chunks of >= 512 rows: multiples of two split-Gram stages (2 x 16) and of the fp32 / bf16 stages
+        nch = gram_chunks(c->T, 32, 1024);     // whole 2 x 16-row split / fp32 stages (bf16: 16)
         x->gpart_elems = (size_t)c->batch * nch * C * 1024;
         x->smat_elems = (size_t)c->batch * C * 1024;
     }
@@ -249,6 +261,7 @@ size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     n += x->smat_elems * (c->gatys && es == 2 ? 6 : 4);     // smat (+ bf16 copy)
     n += (size_t)c->batch * C * 4;                          // spart
     n += 256;                                               // zero line
+    n += (size_t)c->batch * 4;                              // range flags
     n += (size_t)c->batch * x->occ.size() * (c->T / CROWS) * 4;
     const int nf = stft_frames(c->T);
     if (nf) n += 1024 * 8 + (size_t)c->batch * nf * (1 + 1024) * 4;   // STFT regulariser
@@ -402,29 +415,43 @@ const char* ast_last_error(void) { return g_err.c_str(); }
 
 int ast_restore(ast_ctx* x, const char* prefix) {
     if (!x || !prefix) return fail(AST_E_ARG, "ast_restore: null argument");
-    Checkpoint ck;
-    std::string err;
-    if (ck.open(prefix, &err)) return fail(AST_E_NAME, err);
-    std::vector<std::string> names = {"ae_startconv/W", "ae_startconv/biases", "ae_bottleneck/W",
-                                      "ae_bottleneck/biases"};
-    for (int l = 1; l <= 30; ++l)
-        for (const char* k : {"ae_dilatedconv_%d/W", "ae_dilatedconv_%d/biases", "ae_res_%d/W",
-                              "ae_res_%d/biases"}) {
-            char b[64];
-            snprintf(b, sizeof b, k, l);
-            names.push_back(b);
+    try {   // nothing may unwind through the C ABI
+        Checkpoint ck;
+        std::string err;
+        if (ck.open(prefix, &err)) return fail(AST_E_NAME, err);
+        // every encoder variable with the element count its HWIO shape has (masked.py:141-145)
+        std::vector<std::pair<std::string, int64_t>> names = {
+            {"ae_startconv/W", 3 * C}, {"ae_startconv/biases", C}, {"ae_bottleneck/W", C * 16},
+            {"ae_bottleneck/biases", 16}};
+        for (int l = 1; l <= 30; ++l) {
+            const std::pair<const char*, int64_t> ks[4] = {{"ae_dilatedconv_%d/W", 3 * C * C},
+                                                           {"ae_dilatedconv_%d/biases", C},
+                                                           {"ae_res_%d/W", C * C},
+                                                           {"ae_res_%d/biases", C}};
+            for (const auto& k : ks) {
+                char b[64];
+                snprintf(b, sizeof b, k.first, l);
+                names.emplace_back(b, k.second);
+            }
         }
-    std::vector<float> buf;
-    for (const std::string& nm : names) {
-        const CkptEntry* e = ck.find(nm);
-        if (!e) return fail(AST_E_NAME, std::string(prefix) + ": no variable " + nm +
-                                            " (Saver.restore needs every encoder variable)");
-        buf.resize((size_t)e->elements());
-        if (ck.read_f32(*e, buf.data(), &err)) return fail(AST_E_ARG, err);
-        const int rc = ast_set_weight(x, nm.c_str(), buf.data(), buf.size());
-        if (rc) return rc;
+        std::vector<float> buf;
+        for (const auto& nm : names) {
+            const CkptEntry* e = ck.find(nm.first);
+            if (!e) return fail(AST_E_NAME, std::string(prefix) + ": no variable " + nm.first +
+                                                " (Saver.restore needs every encoder variable)");
+            // the shape from the file is checked before anything is allocated for it
+            if (e->elements() != nm.second)
+                return fail(AST_E_NAME, nm.first + ": checkpoint holds " + std::to_string(e->elements()) +
+                                            " elements, the encoder expects " + std::to_string(nm.second));
+            buf.resize((size_t)nm.second);
+            if (ck.read_f32(*e, buf.data(), &err)) return fail(AST_E_ARG, err);
+            const int rc = ast_set_weight(x, nm.first.c_str(), buf.data(), buf.size());
+            if (rc) return rc;
+        }
+        return 0;
+    } catch (const std::exception& ex) {
+        return fail(AST_E_ARG, std::string("ast_restore: ") + ex.what());
     }
-    return 0;
 }
 
 int ast_ot_admm(const double* p_mod, const double* p_ref, int nprob, int n1, int n2, int d,
@@ -503,6 +530,8 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     if (c.gatys && x->bf) ALLOC(x->smatb, x->smat_elems * 2);
     ALLOC(x->zero, 256);
     (void)hipMemset(x->zero, 0, 256);
+    ALLOC(x->rflags, (size_t)c.batch * 4);
+    (void)hipMemset(x->rflags, 0, (size_t)c.batch * 4);
     ALLOC(x->spart, (size_t)c.batch * C * 4);
     x->ncpart = (int)x->occ.size() * (c.T / CROWS);
     ALLOC(x->cpart, (size_t)c.batch * x->ncpart * 4);
@@ -887,10 +916,26 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     // always holds it; its gradient enters grad only through gamma
     launch_stft_reg(xd, x->stft_tw, x->stft_fpart, x->stft_gfr, grad, parts, c.gamma, c.batch,
                     c.T, s);
+    {
+        RangeArgs ra;
+        memset(&ra, 0, sizeof(ra));
+        ra.parts = parts; ra.grad = grad;
+        ra.gmax_e = x->gmax_e; ra.gmax_g = x->gmax_g;
+        ra.split = x->split; ra.nblk = x->nblk; ra.B = c.batch; ra.T = c.T;
+        for (int l = 0; l < NBLK_MAX; ++l) { ra.wdn[l] = x->wdn[l]; ra.bdm[l] = x->bdm[l]; ra.wrn[l] = x->wrn[l]; }
+        ra.flags = x->rflags;
+        launch_range_flags(ra, s);
+    }
     tmark(x, s);
     HIPCHK(hipGetLastError());
     if (x->timing && x->ev_used <= (int)x->ev.size()) x->timed_calls++;
     x->fwd_done = false;   // tapped tensors now hold their gradients, not activations
+    return 0;
+}
+
+int ast_range_flags(ast_ctx* x, int* flags, void* stream) {
+    if (!x || !flags) return fail(AST_E_ARG, "null argument");
+    HIPCHK(hipMemcpyAsync(flags, x->rflags, (size_t)x->cfg.batch * 4, hipMemcpyDeviceToDevice, S(stream)));
     return 0;
 }
 
@@ -923,9 +968,10 @@ int ast_lbfgs_begin(ast_ctx* x, void* ws, float* xd, const double* x0, const int
     if (!x || !ws || !xd) return fail(AST_E_ARG, "null argument");
     if (m < 1 || m > 32) return fail(AST_E_ARG, "L-BFGS-B history m must be in 1..32");
     if (maxiter < 1 || maxls < 1) return fail(AST_E_ARG, "maxiter and maxls must be >= 1");
-    if (!x0 && !x->lb_begun)
+    const bool known = std::find(x->lb_ws.begin(), x->lb_ws.end(), ws) != x->lb_ws.end();
+    if (!x0 && !known)
         return fail(AST_E_STATE, "continuing (x0 NULL) needs a workspace started with x0");
-    x->lb_begun = true;
+    if (x0 && !known) x->lb_ws.push_back(ws);
     launch_lbfgs_begin(ws, xd, x0, active, x->cfg.batch, x->cfg.T, m, maxiter, maxls, ftol, gtol,
                        S(stream));
     HIPCHK(hipGetLastError());
@@ -935,7 +981,8 @@ int ast_lbfgs_begin(ast_ctx* x, void* ws, float* xd, const double* x0, const int
 int ast_lbfgs_step(ast_ctx* x, void* ws, float* xd, const float* grad, const float* parts,
                    void* stream) {
     if (!x || !ws || !xd || !grad || !parts) return fail(AST_E_ARG, "null argument");
-    if (!x->lb_begun) return fail(AST_E_STATE, "ast_lbfgs_begin has not been called");
+    if (std::find(x->lb_ws.begin(), x->lb_ws.end(), ws) == x->lb_ws.end())
+        return fail(AST_E_STATE, "ast_lbfgs_begin (with x0) has not been called on this workspace");
     launch_lbfgs_step(ws, xd, grad, parts, x->cfg.batch, x->cfg.T, S(stream));
     HIPCHK(hipGetLastError());
     return 0;
@@ -943,7 +990,8 @@ int ast_lbfgs_step(ast_ctx* x, void* ws, float* xd, const float* grad, const flo
 
 int ast_lbfgs_state(ast_ctx* x, const void* ws, int* info, double* x64, void* stream) {
     if (!x || !ws || !info) return fail(AST_E_ARG, "null argument");
-    if (!x->lb_begun) return fail(AST_E_STATE, "ast_lbfgs_begin has not been called");
+    if (std::find(x->lb_ws.begin(), x->lb_ws.end(), ws) == x->lb_ws.end())
+        return fail(AST_E_STATE, "ast_lbfgs_begin (with x0) has not been called on this workspace");
     launch_lbfgs_state(ws, info, x64, x->cfg.batch, x->cfg.T, S(stream));
     HIPCHK(hipGetLastError());
     return 0;

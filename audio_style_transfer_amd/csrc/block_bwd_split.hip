@@ -89,9 +89,12 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     // the left neighbour in the same sub-sequence: copied, no MFMAs) or the halo tile's
     // (lane r == 0 -> row 0, r == 1 -> row 1; lanes r >= 2 compute a copy of row 0 and write it
     // to unused row 66).  Other layouts: the tile's columns, no halo rows.
+    // masked layouts have the one-segment geometry (row L = position p0 + L - 1, gathered) and
+    // a tile may start / end inside a sub-sequence: the same halo rows, tap masks in g_a
+    constexpr bool HALO = ONESEG || MASKED;
     int Lv[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) Lv[j] = ONESEG ? Lc[j] + 1 : Lc[j];
+    for (int j = 0; j < 2; ++j) Lv[j] = HALO ? Lc[j] + 1 : Lc[j];
     const int Lh = r == 1 ? 1 : 0;
     const int Lhw = r < 2 ? Lh : TMS + 2;
 
@@ -124,11 +127,11 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         for (int j = 0; j < 2; ++j) {
             // u > 0 of the g_v rows Lv[j]; a position past the clip reads any word (its tot row
             // is zero)
-            const int pv = ONESEG ? min(t.p0 + 1 + 32 * j + r, a.T - 1) : t.p0 + 32 * j + r;
+            const int pv = HALO ? min(t.p0 + 1 + 32 * j + r, a.T - 1) : t.p0 + 32 * j + r;
             mu[j] = a.mu[((size_t)t.b * a.T + pv) * 8 + 4 * h + w];
             me[j] = a.me[(cb + 32 * j + r) * 8 + 4 * h + w];
         }
-        if (ONESEG) {   // rows 0 / 1: p0 - 1 (outside the clip at p0 == 0: its tot row is zero), p0
+        if (HALO) {     // rows 0 / 1: p0 - 1 (outside the clip at p0 == 0: its tot row is zero or tap-masked), p0
             const int p = t.p0 + (r == 1 ? 0 : -1);
             muh = a.mu[((size_t)t.b * a.T + (p < 0 ? 0 : p)) * 8 + 4 * h + w];
         }
@@ -293,7 +296,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         // rows 0 / 1 from the previous tile's rows 64 / 65 when it is the left neighbour (every
         // wave its channel quarter; the previous tile's g_a reads are behind the T barrier, this
         // tile's first writes to rows 64 / 65 come in B)
-        const bool cont = ONESEG && !FIRST && prv.b == cu.b && prv.p0 + TMS == cu.p0 && cu.m0 != 0;
+        const bool cont = HALO && !FIRST && prv.b == cu.b && prv.p0 + TMS == cu.p0 && (MASKED || cu.m0 != 0);
         const int cpo = ((lane >> 2) & 1) * 256 + 64 * w + 16 * (lane & 3);   // (side work of A)
         uint4 cpv = make_uint4(0, 0, 0, 0);
         STAMP(11)
@@ -314,7 +317,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         // max |out| of clip prv.b -> gmax_out once per run of tiles of one clip (omax runs on:
         // with the clip-interleaved tile order a workgroup usually keeps its clip)
         if (!FIRST && cu.b != prv.b) epi_max(prv.b);
-        if (ONESEG && !cont) {
+        if (HALO && !cont) {
             // H: g_v of rows 0 / 1 + g_u of half 1; then g_u of rows 0 / 1
             gemm1(J2{}, [&](int kb) { gu_part(1, kb >> 1, kb & 1, f_u); });
 #pragma unroll

@@ -92,13 +92,14 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     const uint32_t ero = (uint32_t)(lr * RS + 4 * cq);    // + 8 k RS: fp32 row bytes
     // unmasked layouts: byte offset of the unit's source row from the tile's row-0 source
     // (time tb - d); rows without a source (pad rows, rows past the image) read row 1 and are
-    // zeroed (bit k of padz); one-segment halos (unit 0 row 0, unit 8 row 65) are decided per tile
+    // zeroed (bit k of padz); one-segment halos (unit 0 row 0, unit 8 row 65) are decided per
+    // tile.  Masked layouts: only rows past 65 are unused
     uint32_t soff[NU];
     uint32_t padz = 0;
 #pragma unroll
     for (int k = 0; k < NU; ++k) {
         const int L = 8 * k + lr;
-        const bool none = MASKED ? (L == 0 || L > TMS) : (L >= ly.nrows || pad_row(L, ly));
+        const bool none = MASKED ? L > TMS + 1 : (L >= ly.nrows || pad_row(L, ly));
         if (none) padz |= 1u << k;
         soff[k] = MASKED ? 0u : (uint32_t)(((none ? 0 : row_toff(L, ly, a.d)) + a.d) * C * 4 + 4 * cq);
     }
@@ -108,7 +109,10 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     auto load_unit = [&](const Tile& t, int k) {
         if (MASKED) {
             const int L = 8 * k + lr;
-            const int pp = t.p0 + ((padz >> k) & 1u ? 0 : L - 1);
+            // row L = position p0 + L - 1, clamped into the clip (rows 0 / 65 are real
+            // neighbours when the tile starts / ends inside a sub-sequence; the tap masks of
+            // gemm1h drop the ones outside a column's sub-sequence)
+            const int pp = (padz >> k) & 1u ? t.p0 : min(max(t.p0 + L - 1, 0), a.T - 1);
             const float* src = a.ein + ((size_t)t.b * a.T + pos_time(pp, a.fn, a.d)) * C + cq;
             ld[k] = *reinterpret_cast<const float4*>(src);
             return;

@@ -102,7 +102,8 @@ bool parse_block(const uint8_t* b, size_t n, std::vector<std::pair<std::string, 
     while (p < end) {
         uint64_t shared, nonshared, vlen;
         if (!varint(p, end, &shared) || !varint(p, end, &nonshared) || !varint(p, end, &vlen) ||
-            shared > key.size() || (uint64_t)(end - p) < nonshared + vlen) {
+            shared > key.size() || nonshared > (uint64_t)(end - p) ||
+            vlen > (uint64_t)(end - p) - nonshared) {
             *err = "corrupt block entry";
             return false;
         }
@@ -116,7 +117,12 @@ bool parse_block(const uint8_t* b, size_t n, std::vector<std::pair<std::string, 
 }
 
 bool read_block(const std::string& file, const Handle& h, std::string* contents, std::string* err) {
-    if (h.offset + h.size + 5 > file.size()) { *err = "block handle past the end of the index"; return false; }
+    // overflow-safe form of offset + size + 5 (trailer) <= file size: both come from the file
+    const uint64_t fs = file.size();
+    if (h.size > fs || fs - h.size < 5 || h.offset > fs - h.size - 5) {
+        *err = "block handle past the end of the index";
+        return false;
+    }
     const uint8_t* b = (const uint8_t*)file.data() + h.offset;
     const uint8_t type = b[h.size];
     const uint32_t want = fixed32(b + h.size + 1);
@@ -149,12 +155,18 @@ bool parse_entry(const std::string& key, const std::string& val, CkptEntry* e, s
                     const uint8_t* r = g.p;
                     const uint8_t* re = g.p + g.n;
                     Field h;
-                    int64_t size = 0;
+                    uint64_t size = 0;
                     while (r < re) {
                         if (!next_field(r, re, &h)) { *err = "corrupt dim of " + key; return false; }
-                        if (h.num == 1 && h.wire == 0) size = (int64_t)h.v;
+                        if (h.num == 1 && h.wire == 0) size = h.v;
                     }
-                    e->shape.push_back(size);
+                    // a dim is an int64 >= 0; the element count must stay far from overflow
+                    if (size > kMaxElements || e->shape.size() >= 32) {
+                        *err = "implausible shape for " + key;
+                        return false;
+                    }
+                    e->shape.push_back((int64_t)size);
+                    if (e->elements() < 0) { *err = "implausible shape for " + key; return false; }
                 } else if (g.num == 3 && g.wire == 0 && g.v) {
                     *err = "unknown-rank shape for " + key;
                     return false;
@@ -210,7 +222,10 @@ uint32_t crc_mask(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xA282EAD8u; }
 
 int64_t CkptEntry::elements() const {
     int64_t n = 1;
-    for (int64_t d : shape) n *= d;
+    for (int64_t d : shape) {
+        if (d < 0 || (d > 0 && n > kMaxElements / d)) return -1;   // invalid or past the cap
+        n *= d;
+    }
     return n;
 }
 
@@ -254,7 +269,10 @@ int Checkpoint::open(const std::string& pre, std::string* err) {
                 Field f;
                 while (r < re) {
                     if (!next_field(r, re, &f)) { *err = "corrupt bundle header"; return -1; }
-                    if (f.num == 1 && f.wire == 0) num_shards = (int)f.v;
+                    if (f.num == 1 && f.wire == 0) {
+                        if (f.v < 1 || f.v > 99999) { *err = "bad shard count in bundle header"; return -1; }
+                        num_shards = (int)f.v;
+                    }
                     if (f.num == 2 && f.wire == 0 && f.v != 0) {
                         *err = "big-endian checkpoint";
                         return -1;
@@ -288,11 +306,15 @@ int Checkpoint::read_f32(const CkptEntry& e, float* dst, std::string* err) const
         return -1;
     }
     const int64_t n = e.elements();
-    if ((uint64_t)n * eb != e.size) { *err = e.name + ": size does not match shape and dtype"; return -1; }
-    char fn[32];
+    if (n < 0 || (uint64_t)n * eb != e.size) { *err = e.name + ": size does not match shape and dtype"; return -1; }
+    if (e.shard < 0 || e.shard >= num_shards) { *err = e.name + ": shard index out of range"; return -1; }
+    char fn[48];
     std::snprintf(fn, sizeof fn, ".data-%05d-of-%05d", e.shard, num_shards);
     std::ifstream f(prefix + fn, std::ios::binary);
     if (!f) { *err = "cannot read " + prefix + fn; return -1; }
+    f.seekg(0, std::ios::end);
+    const uint64_t fsz = (uint64_t)f.tellg();
+    if (e.offset > fsz || e.size > fsz - e.offset) { *err = e.name + ": data shard shorter than its entry"; return -1; }
     std::vector<uint8_t> buf((size_t)e.size);
     f.seekg((std::streamoff)e.offset);
     if (e.size) f.read((char*)buf.data(), (std::streamsize)e.size);
@@ -327,11 +349,15 @@ extern "C" {
 
 int ast_ckpt_open(const char* prefix, ast_ckpt** out) {
     if (!prefix || !out) return ast::set_error(-1, "ast_ckpt_open: null argument");
-    std::unique_ptr<ast_ckpt> c(new ast_ckpt);
-    std::string err;
-    if (c->ck.open(prefix, &err)) return ast::set_error(-4, err);
-    *out = c.release();
-    return 0;
+    try {   // nothing may unwind through the C ABI (bad_alloc on a hostile file included)
+        std::unique_ptr<ast_ckpt> c(new ast_ckpt);
+        std::string err;
+        if (c->ck.open(prefix, &err)) return ast::set_error(-4, err);
+        *out = c.release();
+        return 0;
+    } catch (const std::exception& ex) {
+        return ast::set_error(-1, std::string("ast_ckpt_open: ") + ex.what());
+    }
 }
 
 void ast_ckpt_close(ast_ckpt* c) { delete c; }
@@ -360,12 +386,16 @@ int ast_ckpt_read_f32(const ast_ckpt* c, const char* name, float* host, size_t n
     if (!c || !name || (!host && n)) return ast::set_error(-1, "ast_ckpt_read_f32: null argument");
     const ast::CkptEntry* e = c->ck.find(name);
     if (!e) return ast::set_error(-4, std::string("ast_ckpt_read_f32: no tensor named ") + name);
-    if ((size_t)e->elements() != n)
+    if (e->elements() < 0 || (size_t)e->elements() != n)
         return ast::set_error(-1, std::string(name) + ": has " + std::to_string(e->elements()) +
                                       " elements, buffer holds " + std::to_string(n));
-    std::string err;
-    if (c->ck.read_f32(*e, host, &err)) return ast::set_error(-1, err);
-    return 0;
+    try {
+        std::string err;
+        if (c->ck.read_f32(*e, host, &err)) return ast::set_error(-1, err);
+        return 0;
+    } catch (const std::exception& ex) {
+        return ast::set_error(-1, std::string("ast_ckpt_read_f32: ") + ex.what());
+    }
 }
 
 }  // extern "C"

@@ -15,6 +15,10 @@
 
 namespace ast {
 
+// largest element count a tensor entry may declare (2^40: far above any encoder variable,
+// far below int64 overflow of elements x bytes)
+constexpr int64_t kMaxElements = (int64_t)1 << 40;
+
 enum CkptDtype { CK_FLOAT = 1, CK_DOUBLE = 2, CK_INT32 = 3, CK_INT64 = 9, CK_BF16 = 14, CK_HALF = 19 };
 
 struct CkptEntry {
@@ -26,7 +30,7 @@ struct CkptEntry {
     uint32_t crc = 0;
     bool has_crc = false;
     bool sliced = false;
-    int64_t elements() const;
+    int64_t elements() const;   // -1 for a negative dim or a count above kMaxElements
 };
 
 struct Checkpoint {

@@ -304,6 +304,16 @@ constexpr int CROWS = 64;   // rows per content workgroup
 void launch_finalize(float* parts, const float* cpart, int ncpart, float cscale,
                      const float* spart, int nspart, float sscale, float lambd, int B,
                      hipStream_t s);
+// per-clip range / finiteness flags of one loss+grad evaluation (gram.hip, ast_range_flags)
+struct RangeArgs {
+    const float* parts; const float* grad;  // [B][4], [B][T]
+    const unsigned* gmax_e; const unsigned* gmax_g;   // split: [nblk + 1][B] per-clip maxima
+    int split, nblk, B, T;
+    float wdn[30], bdm[30], wrn[30];        // split: the per-block operand bounds (splitwave.h)
+    int* flags;                             // [B]
+};
+void launch_range_flags(const RangeArgs& a, hipStream_t s);
+
 // b^n by squaring: the same fp32 products on host and device, so the host-counter and the
 // device-counter Adam steps agree bit for bit
 __host__ __device__ inline float pow_int(float b, int n) {

@@ -231,6 +231,44 @@ __global__ void __launch_bounds__(256) k_finalize(float* parts, const float* cpa
     }
 }
 
+// Per-clip flags (include/astyle.h AST_RANGE_*): non-finite loss parts or gradient; in split
+// mode also every per-clip maximum the split-fp16 scales were derived from (splitwave.h
+// scale_exp: in range for maxima in [2^-47, 2^74)) and the analytic intermediate bounds
+// |u| <= wdn max|e_l| + bdm, |W_r tot| <= wrn max|tot|: beyond 2^74 the scaled halves would
+// overflow fp16; below 2^-60 they lose significand bits.
+__global__ void __launch_bounds__(256) k_range_flags(RangeArgs a) {
+    const int b = blockIdx.x, tid = threadIdx.x;
+    bool bad = false;
+    for (int i = tid; i < a.T; i += 256) bad |= !isfinite(a.grad[(size_t)b * a.T + i]);
+    if (tid < 4) bad |= !isfinite(a.parts[b * 4 + tid]);
+    bad = __syncthreads_or(bad);
+    if (tid) return;
+    int f = bad ? 1 : 0;
+    if (a.split) {
+        const float hi = 0x1p74f, lo = 0x1p-60f;
+        auto chk = [&](float m, int bit) {
+            if (!(m < hi)) f |= bit;
+            else if (m > 0.f && m < lo) f |= 8;
+        };
+        for (int t = 0; t <= a.nblk; ++t) {
+            const float ge = __uint_as_float(a.gmax_e[(size_t)t * a.B + b]);
+            const float gg = __uint_as_float(a.gmax_g[(size_t)t * a.B + b]);
+            chk(ge, 2);
+            chk(gg, 4);
+            if (t < a.nblk) {
+                if (!(fmaf(a.wdn[t], ge, a.bdm[t]) < hi)) f |= 2;
+                const float gn = __uint_as_float(a.gmax_g[(size_t)(t + 1) * a.B + b]);
+                if (!(a.wrn[t] * gn < hi)) f |= 4;
+            }
+        }
+    }
+    a.flags[b] = f;
+}
+
+void launch_range_flags(const RangeArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_range_flags, dim3(a.B), dim3(256), 0, s, a);
+}
+
 void launch_style_ours(const StyleArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_style_ours, dim3(a.B * (C / 4)), dim3(256), 0, s, a);
 }

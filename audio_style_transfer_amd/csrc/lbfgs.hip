@@ -52,7 +52,8 @@ constexpr int LB_MAGIC = 0x4c42464d;
 constexpr size_t LB_HDR = 512;
 
 // reasons (ast_lbfgs_state)
-enum { LB_RUNNING = 0, LB_STOP_ITER = 1, LB_CONV_PGTOL = 2, LB_CONV_REL_F = 3, LB_ABNORMAL = 4 };
+enum { LB_RUNNING = 0, LB_STOP_ITER = 1, LB_CONV_PGTOL = 2, LB_CONV_REL_F = 3, LB_ABNORMAL = 4,
+       LB_BAD_WORKSPACE = 5 };
 
 namespace {
 
@@ -334,11 +335,18 @@ struct StepArgs {
 };
 
 __device__ __forceinline__ int ws_m(const void* ws) { return ((const LbHeader*)ws)->m; }
+// the workspace was started (ast_lbfgs_begin with x0) for this B and T, with a valid m: no
+// launch indexes a workspace through a header it did not write
+__device__ __forceinline__ bool ws_ok(const void* ws, int B, int T) {
+    const LbHeader h = *(const LbHeader*)ws;
+    return h.magic == LB_MAGIC && h.m >= 1 && h.m <= LB_MMAX && h.B == B && h.T == T;
+}
 
 __global__ void __launch_bounds__(NT) k_lbfgs_step(StepArgs a) {
     __shared__ double red[NT / 64];
     __shared__ double alpha[LB_MMAX];
     const int b = blockIdx.x, T = a.T;
+    if (!ws_ok(a.ws, a.B, T)) return;   // never started: nothing to advance (state reports it)
     const Ws w = ws_view(a.ws, a.B, T, ws_m(a.ws), b);
     LbState s = *w.st;
     if (s.phase == 0) return;
@@ -435,6 +443,7 @@ __global__ void __launch_bounds__(NT) k_lbfgs_begin(void* ws, float* x, const do
                                                     int maxiter, int maxls, double tol,
                                                     double pgtol) {
     const int b = blockIdx.x;
+    if (!x0 && !ws_ok(ws, B, T)) return;   // a continuation needs a started workspace
     if (!x0) m = ws_m(ws);   // a continuation keeps the workspace's own history size
     const Ws w = ws_view(ws, B, T, m, b);
     LbState s = *w.st;
@@ -460,6 +469,13 @@ __global__ void __launch_bounds__(NT) k_lbfgs_begin(void* ws, float* x, const do
 
 __global__ void k_lbfgs_state(const void* ws, int* info, double* x64, int B, int T) {
     const int b = blockIdx.x;
+    if (!ws_ok(ws, B, T)) {            // not a started workspace of this B, T: say so
+        if (threadIdx.x == 0) {
+            info[b * 4 + 0] = 0; info[b * 4 + 1] = 0; info[b * 4 + 2] = 0;
+            info[b * 4 + 3] = LB_BAD_WORKSPACE;
+        }
+        return;
+    }
     const Ws w = ws_view(const_cast<void*>(ws), B, T, ws_m(ws), b);
     const LbState& s = *w.st;
     if (threadIdx.x == 0) {

@@ -125,7 +125,9 @@ __device__ __forceinline__ bool pad_row(int L, const Layout& ly) {
 //      unit as the tile's row-0 source (time tb - d) + a constant per-lane byte offset; rows
 //      without a source (pad rows, rows past the image, a one-segment halo at a sub-sequence
 //      end) read a row of the tile and are zeroed at conversion (zero bit k).  Masked layouts
-//      gather per lane (rows 0 and 65 have no source). ----
+//      gather per lane: row L is position p0 + L - 1 (clamped into the clip; a tile may start
+//      or end inside a sub-sequence, so rows 0 and 65 can be real neighbours), and the
+//      per-column tap masks drop every neighbour outside the column's sub-sequence. ----
 constexpr int NU = 9;
 template <bool MASKED, bool ONESEG>
 struct RowUnits {
@@ -144,7 +146,7 @@ struct RowUnits {
 #pragma unroll
         for (int k = 0; k < NU; ++k) {
             const int L = 8 * k + lr;
-            const bool none = MASKED ? (L == 0 || L > TMS) : (L >= ly.nrows || pad_row(L, ly));
+            const bool none = MASKED ? L > TMS + 1 : (L >= ly.nrows || pad_row(L, ly));
             if (none) padz |= 1u << k;
             soff[k] = MASKED ? 0u : (uint32_t)(((none ? 0 : row_toff(L, ly, d)) + d) * C * 4 + 4 * cq);
         }
@@ -155,7 +157,7 @@ struct RowUnits {
     __device__ __forceinline__ float4 load(const float* src, const Tile& t, int k, int T, const FDiv& fn, int d) const {
         if (MASKED) {
             const int L = 8 * k + lr;
-            const int pp = t.p0 + ((padz >> k) & 1u ? 0 : L - 1);
+            const int pp = (padz >> k) & 1u ? t.p0 : min(max(t.p0 + L - 1, 0), T - 1);
             return *reinterpret_cast<const float4*>(src + ((size_t)t.b * T + pos_time(pp, fn, d)) * C + cq);
         }
         const char* base = reinterpret_cast<const char*>(src + ((ptrdiff_t)t.b * T + t.tb - d) * C);

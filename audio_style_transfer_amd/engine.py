@@ -191,6 +191,14 @@ class StyleEngine:
                                               float(beta1), float(beta2), float(eps),
                                               self._stream()))
 
+    def range_flags(self) -> torch.Tensor:
+        """Per-clip AST_RANGE_* flags [B] (int32, device) of the last loss_grad: non-finite
+        loss parts or gradient (1); in split mode a per-clip maximum or analytic operand bound
+        outside the split-fp16 range (2: forward, 4: backward) or below 2^-60 (8)."""
+        out = torch.empty(self.batch, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.ast_range_flags(self.h, self._ptr(out, torch.int32), self._stream()))
+        return out
+
     @staticmethod
     def nonfinite_clips(parts: torch.Tensor, grad: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Per-clip flag [B] (bool, on the device): the clip's loss parts or its gradient hold a

@@ -152,8 +152,14 @@ class GatysNet(object):
         history = []
         start_ep = 0
         ckpt = os.path.join(self.savepath, 'state.npz')
+        fp = self._run_fingerprint(phi_c, phi_s, lambd, gamma, optimizer)
         if resume and os.path.isfile(ckpt):
             with np.load(ckpt, allow_pickle=False) as z:
+                saved = str(z['fingerprint']) if 'fingerprint' in z.files else None
+                if saved != fp:
+                    raise ValueError('%s was saved by a different run (targets, lambd, gamma, '
+                                     'length, taps, precision or optimizer differ); refusing to '
+                                     'resume from it' % ckpt)
                 x = np.asarray(z['x'], dtype=np.float64)
                 start_ep, state['i_'] = int(z['ep']) + 1, int(z['i_'])
             log('resuming after epoch %d (%d evaluations) from %s' % (start_ep, state['i_'], ckpt))
@@ -201,7 +207,8 @@ class GatysNet(object):
                     ep + 1, epochs, state['i'], time.time() - state['since'], *p))
             state['i_'] = state['i']
             writer.flush()
-            np.savez(ckpt, x=x.astype(np.float32).astype(np.float64), ep=ep, i_=state['i_'])
+            np.savez(ckpt, x=x.astype(np.float32).astype(np.float64), ep=ep, i_=state['i_'],
+                     fingerprint=np.array(fp))
             audio = utils.inv_mu_law_numpy(x[None])[0, self.late:-self.late]
             sp = os.path.join(self.savepath, 'ep-{}.wav'.format(ep))
             utils.write_wav(sp, audio / np.max(audio), sr=self.sr)        # methods.py:176
@@ -214,6 +221,18 @@ class GatysNet(object):
         writer.close()
         self.history = history
         return x
+
+    def _run_fingerprint(self, phi_c, phi_s, lambd, gamma, optimizer):
+        """What a saved epoch state depends on: the targets (hence the content / style files and
+        the weights), the loss constants, the clip length, the taps, precision and optimiser."""
+        import hashlib
+        h = hashlib.sha256()
+        for a in (phi_c, phi_s):
+            h.update(np.ascontiguousarray(np.asarray(a, dtype=np.float32)).tobytes())
+        h.update(repr((float(lambd), float(gamma), int(self.batch_size), self.cont_lyr_ids,
+                       self.style_lyr_ids, self.nb_channels, self.cnt_channels, bool(self.gatys),
+                       self.precision, optimizer)).encode())
+        return h.hexdigest()
 
     def run(self, cont_file, source, target, epochs, lambd=0.1, gamma=0.1, audio_channel=0,
             start=1.0, resume=False):

@@ -57,3 +57,43 @@ def synthetic_clips(n: int, T: int, seed0: int, sr: int = 16000):
         s = s + 0.05 * rng.standard_normal(T)
         out[b] = 0.9 * s / np.max(np.abs(s))
     return out
+
+
+STRESS_KINDS = ('dr4', 'dr025', 'alt2', 'student_t', 'bias100')
+
+
+def stressed_weights(kind: str, seed: int = 0):
+    """Weight sets whose statistics differ from uniform_unit_scaling, for range tests of the
+    split-fp16 mode (per-block weight exponents, analytic operand bounds; splitwave.h):
+      dr4        every block's W_d x 4, W_r x 0.25 (u 4x wider, per-block exponents shift)
+      dr025      W_d x 0.25, W_r x 4
+      alt2       blocks alternately x 2 / x 0.5 (both W): max |e| grows to ~3e5 by block 30
+      student_t  heavy-tailed W ~ Student-t(3) at the same variance (max |W| ~ 9, not 1)
+      bias100    biases x 100 (activations ~1e3)"""
+    import re
+    W = synthetic_weights(seed)
+    if kind == 'student_t':
+        rng = np.random.Generator(np.random.PCG64(seed + 7))
+        out = {}
+        for name, v in W.items():
+            if name.endswith('/W'):
+                fan_in = int(np.prod(v.shape[:-1]))
+                t = rng.standard_t(3, size=v.shape) / np.sqrt(3.0)      # unit variance
+                out[name] = (t * np.sqrt(1.0 / fan_in)).astype(np.float32)
+            else:
+                out[name] = v
+        return out
+    out = {}
+    for name, v in W.items():
+        m = re.match(r'ae_(dilatedconv|res)_(\d+)/W$', name)
+        f = 1.0
+        if kind == 'bias100':
+            f = 100.0 if name.endswith('/biases') else 1.0
+        elif m:
+            conv, l = m.group(1) == 'dilatedconv', int(m.group(2))
+            f = {'dr4': 4.0 if conv else 0.25, 'dr025': 0.25 if conv else 4.0,
+                 'alt2': 2.0 if l % 2 == 0 else 0.5}[kind]
+        elif kind not in STRESS_KINDS:
+            raise ValueError('unknown stress kind %r' % kind)
+        out[name] = (v * np.float32(f)).astype(np.float32)
+    return out

@@ -97,6 +97,23 @@ int ast_set_targets(ast_ctx* ctx, const float* phi_c_dev, int phi_c_shared,
  * whatever gamma is, and enters the gradient only through gamma. */
 int ast_loss_grad(ast_ctx* ctx, const float* x_dev, float* grad_dev, float* parts_dev, void* stream);
 
+/* Per-clip flags of the last ast_loss_grad into flags_dev [batch] (int, device), OR of:
+ *   AST_RANGE_NONFINITE  the clip's loss parts or gradient hold a NaN / Inf (the reference
+ *                        would hand them to the next L-BFGS-B step);
+ *   AST_RANGE_ACT        precision 2: a per-clip max |e_l| or the forward intermediate bound
+ *                        wdn max|e_l| + bdm (splitwave.h) is >= 2^74 or not finite, so the
+ *                        power-of-two scale that keeps the split-fp16 halves in range clamps;
+ *   AST_RANGE_GRAD       precision 2: the same for the backward chain max |d loss / d e_l| and
+ *                        its bound wrn max|tot|;
+ *   AST_RANGE_TINY       precision 2: some per-clip max is below 2^-60 (the halves of that
+ *                        tensor lose significand bits; results stay finite).
+ * 0 = the evaluation is within the split representation's range.  Graph-capturable. */
+#define AST_RANGE_NONFINITE 1
+#define AST_RANGE_ACT 2
+#define AST_RANGE_GRAD 4
+#define AST_RANGE_TINY 8
+int ast_range_flags(ast_ctx* ctx, int* flags_dev, void* stream);
+
 /* Change gamma (methods.py:125) without rebuilding the context. */
 int ast_set_gamma(ast_ctx* ctx, float gamma);
 
@@ -120,7 +137,9 @@ int ast_adam_step_dev(ast_ctx* ctx, float* x_dev, float* m_dev, float* v_dev, co
  * current point with the workspace's own m, the next epoch of methods.py:164);
  * active_dev [batch] int (NULL = all) selects the clips that run.  info_dev [batch, 4] =
  * (phase, iterations, evaluations, reason: 0 running, 1 maxiter, 2 pgtol, 3 rel. reduction
- * of f, 4 abnormal line search); x64_dev [batch, T] (may be NULL) the current float64 point.
+ * of f, 4 abnormal line search, 5 the workspace header is not one begin wrote for this batch
+ * and T); x64_dev [batch, T] (may be NULL) the current float64 point.  step / state / a
+ * continuation on a workspace this context never started with x0 fail with AST_E_STATE.
  * begin/step allocate nothing, so the step pair is hipGraph-capturable. */
 int ast_lbfgs_workspace_bytes(ast_ctx* ctx, int m, size_t* out_bytes);
 int ast_lbfgs_begin(ast_ctx* ctx, void* ws_dev, float* x_dev, const double* x0_dev,

@@ -41,22 +41,24 @@ def loss_fn(x, W, *, cont_ids, style_ids, phi_c, phi_s, lambd=100.0, gamma=0.0, 
     """x: torch [T] (requires_grad).  Returns (total, content, style, reg)."""
     h = (x / 128.0)[None, None, :].to(dtype)
     e = _conv(h, _w(W, 'ae_startconv/W', dtype), _w(W, 'ae_startconv/biases', dtype), 1)
-    ext = []
+    ext = []                                              # extracts as [C, T] (conv1d layout)
     for l in range(n_blocks):
         d = 2 ** (l % 10)
         u = _conv(torch.relu(e), _w(W, 'ae_dilatedconv_%d/W' % (l + 1), dtype),
                   _w(W, 'ae_dilatedconv_%d/biases' % (l + 1), dtype), d)
         e = e + _conv(torch.relu(u), _w(W, 'ae_res_%d/W' % (l + 1), dtype),
                       _w(W, 'ae_res_%d/biases' % (l + 1), dtype), 1)
-        ext.append(e[0].T)                                # [T, C]
+        ext.append(e[0])                                  # [C, T]
     if n_blocks == 30:
         ext.append(ext[-1])
         bott = _conv(e, _w(W, 'ae_bottleneck/W', dtype), _w(W, 'ae_bottleneck/biases', dtype), 1)
-        ext.append(bott[0].T)
-    emb = torch.cat([ext[i][:, :cnt_channels] for i in cont_ids], dim=1)
-    content = 10.0 * torch.mean((emb - torch.as_tensor(phi_c, dtype=dtype)) ** 2)
-    stl = torch.stack([ext[i] for i in style_ids], 0)     # [L, T, C]
-    s = stl.permute(2, 0, 1) if not gatys else stl.permute(0, 2, 1)
+        ext.append(bott[0])
+    # methods.py:58: content taps [T, n cnt] (kept transposed: [n cnt, T])
+    emb = torch.cat([ext[i][:cnt_channels] for i in cont_ids], dim=0)
+    content = 10.0 * torch.mean((emb - torch.as_tensor(phi_c, dtype=dtype).T) ** 2)
+    # methods.py:60-73: ours G_c = E_c E_c^T over [C, L, T]; Gatys G_l = F_l F_l^T over [L, C, T]
+    stl = torch.stack([ext[i] for i in style_ids], 0)     # [L, C, T]
+    s = stl.permute(1, 0, 2).contiguous() if not gatys else stl
     G = s @ s.transpose(1, 2)
     ss = (G * G).sum(dim=(1, 2), keepdim=True)
     Gn = G * torch.rsqrt(torch.clamp(ss, min=1e-12))

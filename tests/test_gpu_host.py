@@ -170,7 +170,7 @@ def test_event_log_and_resume(tmp_path, weights):
     st = np.load(str(out / 'state.npz'))
     assert int(st['ep']) == 0 and int(st['i_']) == len(h) and np.array_equal(st['x'], x1)
     # pretend epoch 0 used 60 evaluations (no early stop), then resume into epoch 1
-    np.savez(str(out / 'state.npz'), x=x1, ep=0, i_=60)
+    np.savez(str(out / 'state.npz'), x=x1, ep=0, i_=60, fingerprint=st['fingerprint'])
     x2 = net.l_bfgs(phi_c, phi_s, epochs=2, lambd=100.0, gamma=0.0, maxiter=4, resume=True,
                     log=lambda s: None)
     assert os.path.isfile(out / 'ep-1.wav')
@@ -184,3 +184,8 @@ def test_event_log_and_resume(tmp_path, weights):
     # a finished run (last epoch stopped early) resumes to its saved point without evaluating
     x4 = net.l_bfgs(phi_c, phi_s, epochs=5, lambd=100.0, gamma=0.0, resume=True, log=lambda s: None)
     assert np.array_equal(x4, x3) and net.history == []
+    # a state saved by another run (other lambd / targets) is refused, not silently continued
+    with pytest.raises(ValueError):
+        net.l_bfgs(phi_c, phi_s, epochs=5, lambd=10.0, gamma=0.0, resume=True, log=lambda s: None)
+    with pytest.raises(ValueError):
+        net.l_bfgs(phi_c * 2, phi_s, epochs=5, lambd=100.0, gamma=0.0, resume=True, log=lambda s: None)

@@ -84,10 +84,12 @@ def test_split_loss_grad_matches_oracle(tag, weights, golden, dev):
     assert e <= 2e-3
 
 
-@pytest.mark.parametrize('T', [512, 1024, 2048])
+@pytest.mark.parametrize('T', [512, 1024, 2048, 3584])
 def test_split_extracts_match_oracle(T, weights, dev):
     """Every dilation layout of the split kernels: one segment with halo rows (n >= 64),
-    32-position segments with pad rows (n == 32), per-column tap masks (n < 32)."""
+    32-position segments with pad rows (n == 32), per-column tap masks (n < 32; and at
+    T = 3584, n = 224 / 112 / 56 / 28 / 14 / 7, where a 64-position tile starts and ends inside
+    a sub-sequence)."""
     kw = dict(CASES['trunc'], cont_ids=[29, 31], style_ids=[0, 30])
     x = O.mu_law_numpy(synthetic_clips(1, T, 42)[0]) + np.random.default_rng(3).normal(0, 4, T)
     ext, _ = O.encoder_forward(x, weights, 30, need_bottleneck=True)
@@ -152,12 +154,57 @@ def test_split_batch_invariance_and_determinism(weights, dev):
         assert torch.equal(p1[0], p3[b]) and torch.equal(g1[0], g3[b]), b
 
 
-@pytest.mark.parametrize('precision', ['split', 'bf16'])
-def test_bench_size_batch(precision, weights, dev):
-    """configs[2] at its size: B = 256 clips of T = 16384.  Four clip slots (first, last, two
-    inside) are bit-identical to a B = 1 run of the same clip, and one matches the oracle."""
+@pytest.mark.parametrize('tag,precision', [('gatys', 'split'), ('gatys', 'fp32')])
+def test_gatys_full_size(tag, precision, weights, dev):
+    """configs[4]'s clip: T = 16384, all 30 blocks, Gatys Gram [30, 128, 128] (methods.py:68-74
+    with --gatys) vs the oracle, in the headline split mode and in fp32 mode."""
+    T = 16384
+    kw = CASES[tag]
+    phi_c, phi_s = _targets(tag, T, weights)
+    x = O.mu_law_numpy(synthetic_clips(1, T, 42)[0]) + np.random.default_rng(5).normal(0, 4, T)
+    ref_parts, ref_g = O.loss_and_grad(x, weights, phi_c=phi_c, phi_s=phi_s, lambd=100.0, **kw)
+    eng = _engine(1, T, kw, weights, precision)
+    _set(eng, tag, T, weights)
+    parts, grad = eng.loss_grad(torch.tensor(x[None], dtype=torch.float32, device=dev))
+    parts, grad = parts.cpu().numpy()[0], grad.cpu().numpy()[0]
+    for k in range(3):
+        assert abs(parts[k] - ref_parts[k]) <= 1e-4 * abs(ref_parts[k]) + 1e-7, (k, parts, ref_parts)
+    e = rel(grad, ref_g)
+    print('gatys %s T=16384 grad rel-L2 %.3g' % (precision, e))
+    assert e <= 2e-3
+
+
+@pytest.mark.parametrize('T,tag,precision', [(3584, 'ours', 'split'), (3584, 'ours', 'fp32'),
+                                             (12800, 'gatys', 'split'), (12800, 'gatys', 'fp32')])
+def test_odd_lengths_match_oracle(T, tag, precision, weights, dev):
+    """Clip lengths whose Gram time chunks are not powers of two (T / 1024 = 3 chunks would not
+    divide T = 3584 into whole stages; T / 4096 = 3 would drop rows of T = 12800): every row of
+    every chunk is counted once, and D lands on its own rows only."""
+    kw = dict(CASES[tag], cont_ids=[29])
+    xc = O.mu_law_numpy(synthetic_clips(1, T, 1000)[0])
+    xs = O.mu_law_numpy(synthetic_clips(1, T, 5000)[0])
+    phi_c, phi_s = O.targets_from_audio(weights, xc, [xs], [xc], **kw)
+    x = xc + np.random.default_rng(8).normal(0, 4, T)
+    ref_parts, ref_g = O.loss_and_grad(x, weights, phi_c=phi_c, phi_s=phi_s, lambd=100.0, **kw)
+    eng = _engine(2, T, kw, weights, precision)
+    eng.set_targets(torch.tensor(phi_c, dtype=torch.float32), torch.tensor(phi_s, dtype=torch.float32))
+    parts, grad = eng.loss_grad(torch.tensor(np.stack([x, x]), dtype=torch.float32, device=dev))
+    parts, grad = parts.cpu().numpy(), grad.cpu().numpy()
+    assert np.array_equal(parts[0], parts[1]) and np.array_equal(grad[0], grad[1])
+    for k in range(3):
+        assert abs(parts[0][k] - ref_parts[k]) <= 1e-4 * abs(ref_parts[k]) + 1e-7, (k, parts[0], ref_parts)
+    e = rel(grad[0], ref_g)
+    print('T=%d %s %s grad rel-L2 %.3g' % (T, tag, precision, e))
+    assert e <= 2e-3
+
+
+@pytest.mark.parametrize('tag,precision', [('ours', 'split'), ('ours', 'bf16'), ('gatys', 'split')])
+def test_bench_size_batch(tag, precision, weights, dev):
+    """configs[2] (ours) and configs[4] (--gatys) at their size: B = 256 clips of T = 16384.
+    Four clip slots (first, last, two inside) are bit-identical to a B = 1 run of the same
+    clip, and one matches the oracle."""
     B, T = 256, 16384
-    kw = dict(CASES['ours'], cont_ids=[29])
+    kw = dict(CASES[tag], cont_ids=[29])
     phi_c, phi_s = O.targets_from_audio(weights, O.mu_law_numpy(synthetic_clips(1, T, 1000)[0]),
                                         [O.mu_law_numpy(synthetic_clips(1, T, 5000)[0])],
                                         [O.mu_law_numpy(synthetic_clips(1, T, 1000)[0])], **kw)
@@ -185,7 +232,7 @@ def test_bench_size_batch(precision, weights, dev):
         for k in range(3):
             assert abs(float(pB[97, k]) - ref_parts[k]) <= 1e-4 * abs(ref_parts[k]) + 1e-7
         e = rel(gB[97].numpy(), ref_g)
-        print('B=256 slot 97 split grad rel-L2 %.3g' % e)
+        print('B=256 slot 97 %s split grad rel-L2 %.3g' % (tag, e))
         assert e <= 2e-3
 
 
@@ -224,3 +271,51 @@ def test_split_scale_range(weights, dev):
         e = rel(grad.cpu().numpy()[0], ref_g)
         print('x scale %.3g: grad rel-L2 %.3g' % (np.abs(x).max(), e))
         assert e <= 2e-3
+
+
+@pytest.mark.parametrize('kind', ['dr4', 'dr025', 'alt2', 'student_t', 'bias100'])
+def test_split_weight_statistics(kind, dev):
+    """The split mode's range management (per-block weight exponents; the analytic bounds
+    |u| <= wdn max|e| + bdm and |W_r tot| <= wrn max|tot| that set the intermediates' scales)
+    under weight sets unlike uniform_unit_scaling — W_d / W_r scaled x4 / x0.25, blocks
+    alternately x2 / x0.5, heavy-tailed Student-t(3) weights, biases x100 — held to the fp32
+    bars against the fp64 oracle, the fp32 mode beside it, and no clip flagged."""
+    from audio_style_transfer_amd.weights import stressed_weights
+    T = 2048
+    W = stressed_weights(kind)
+    kw = dict(CASES['ours'], cont_ids=[29])
+    xc = O.mu_law_numpy(synthetic_clips(1, T, 1000)[0])
+    xs = O.mu_law_numpy(synthetic_clips(1, T, 5000)[0])
+    phi_c, phi_s = O.targets_from_audio(W, xc, [xs], [xc], **kw)
+    x = xc + np.random.default_rng(6).normal(0, 4, T)
+    ref_parts, ref_g = O.loss_and_grad(x, W, phi_c=phi_c, phi_s=phi_s, lambd=100.0, **kw)
+    errs = {}
+    for precision in ('split', 'fp32'):
+        eng = _engine(1, T, kw, W, precision)
+        eng.set_targets(torch.tensor(phi_c, dtype=torch.float32), torch.tensor(phi_s, dtype=torch.float32))
+        parts, grad = eng.loss_grad(torch.tensor(x[None], dtype=torch.float32, device=dev))
+        flags = eng.range_flags().cpu().numpy()
+        parts = parts.cpu().numpy()[0]
+        assert flags[0] == 0, (precision, flags)
+        for k in range(3):
+            assert abs(parts[k] - ref_parts[k]) <= 1e-4 * abs(ref_parts[k]) + 1e-7, (precision, k, parts, ref_parts)
+        errs[precision] = rel(grad.cpu().numpy()[0], ref_g)
+        eng.close()
+    print('%s: grad rel-L2 split %.3g, fp32 %.3g' % (kind, errs['split'], errs['fp32']))
+    assert errs['split'] <= 2e-3
+
+
+def test_range_flags(weights, dev):
+    """ast_range_flags: 0 on ordinary inputs; a clip driven past the split representation
+    (x ~ 1e30: max |e_0| ~ 1e28 > 2^74) is flagged, its neighbour is not."""
+    T = 1024
+    kw = CASES['c1']
+    eng = _engine(2, T, kw, weights)
+    _set(eng, 'c1', T, weights)
+    x = O.mu_law_numpy(synthetic_clips(2, T, 77))
+    eng.loss_grad(torch.tensor(x, dtype=torch.float32, device=dev))
+    assert eng.range_flags().cpu().tolist() == [0, 0]
+    x[1] = 1e30
+    eng.loss_grad(torch.tensor(x, dtype=torch.float32, device=dev))
+    f = eng.range_flags().cpu().tolist()
+    assert f[0] == 0 and f[1] & 2, f

@@ -71,7 +71,9 @@ def entry_proto(dtype, shape, shard, offset, size, crc):
 
 def write_checkpoint(prefix, tensors, num_shards=1, block_size=4096, restart=16,
                      corrupt=None):
-    """tensors: {name: ndarray}.  Tensors are spread over shards round-robin in name order."""
+    """tensors: {name: ndarray}.  Tensors are spread over shards round-robin in name order.
+    Returns the .index layout: [(offset, size)] of every table block (without its 5-byte
+    trailer), data blocks first, then the metaindex and the index block."""
     names = sorted(tensors)
     shards = [bytearray() for _ in range(num_shards)]
     kv = [(b'', _field(1, 0) + _varint(num_shards) + _bytes_field(3, _field(1, 0) + _varint(1)))]
@@ -94,12 +96,15 @@ def write_checkpoint(prefix, tensors, num_shards=1, block_size=4096, restart=16,
     cur = []
     size = 0
 
+    blocks = []
+
     def flush():
         nonlocal cur, size
         if not cur:
             return
         blk = _block(cur, restart)
         index.append((cur[-1][0], len(out), len(blk)))
+        blocks.append((len(out), len(blk)))
         out.extend(_with_trailer(blk))
         cur, size = [], 0
     for k, v in kv:
@@ -110,9 +115,11 @@ def write_checkpoint(prefix, tensors, num_shards=1, block_size=4096, restart=16,
     flush()
     meta = _block([], restart)
     meta_h = (len(out), len(meta))
+    blocks.append(meta_h)
     out.extend(_with_trailer(meta))
     iblk = _block([(k, _varint(o) + _varint(n)) for k, o, n in index], 1)
     index_h = (len(out), len(iblk))
+    blocks.append(index_h)
     out.extend(_with_trailer(iblk))
     foot = _varint(meta_h[0]) + _varint(meta_h[1]) + _varint(index_h[0]) + _varint(index_h[1])
     foot = foot + bytes(40 - len(foot))
@@ -125,3 +132,11 @@ def write_checkpoint(prefix, tensors, num_shards=1, block_size=4096, restart=16,
         out[5] ^= 0x40
     with open(prefix + '.index', 'wb') as f:
         f.write(bytes(out))
+    return blocks
+
+
+def retrailer(index: bytearray, off: int, size: int) -> None:
+    """Recompute the masked CRC-32C trailer of the block at [off, off + size) in place (its type
+    byte included), so a mutated block passes the CRC check and reaches the parser."""
+    index[off + size + 1:off + size + 5] = _with_trailer(bytes(index[off:off + size]),
+                                                          index[off + size])[-4:]
