@@ -458,14 +458,26 @@ int ast_ot_admm(const double* p_mod, const double* p_ref, int nprob, int n1, int
                 double eps, double miter, double* plan, double* pal, int* iters, void* stream) {
     if (nprob < 0 || n1 < 1 || n2 < 1 || d < 1)
         return fail(AST_E_ARG, "ast_ot_admm: need nprob >= 0 and n1, n2, d >= 1");
-    if ((long long)n1 * n2 > ot_max_cells())
-        return fail(AST_E_ARG, "ast_ot_admm: n1 * n2 must be <= " + std::to_string(ot_max_cells()));
+    if ((long long)n1 * n2 > (1ll << 26) || ot_big_lds_bytes(n1, n2) > 160 * 1024)
+        return fail(AST_E_ARG, "ast_ot_admm: n1 * n2 must be <= 2^26 and n1 + n2 <= 20000");
     if (!(eps > 0.0) || !(miter >= 0.0))
         return fail(AST_E_ARG, "ast_ot_admm: eps must be > 0 and miter >= 0");
     if (nprob == 0) return 0;
     if (!p_mod || !p_ref || !plan) return fail(AST_E_ARG, "ast_ot_admm: null buffer");
-    launch_ot_admm(p_mod, p_ref, nprob, n1, n2, d, eps, miter, plan, pal, iters, S(stream));
-    HIPCHK(hipGetLastError());
+    if ((long long)n1 * n2 <= ot_max_cells()) {
+        launch_ot_admm(p_mod, p_ref, nprob, n1, n2, d, eps, miter, plan, pal, iters, S(stream));
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
+    // larger palettes: iterates in a stream-ordered device workspace (allocated and freed on
+    // the call's stream)
+    void* ws = nullptr;
+    HIPCHK(hipMallocAsync(&ws, ot_big_ws_bytes(n1, n2) * (size_t)nprob, S(stream)));
+    launch_ot_admm_big(p_mod, p_ref, nprob, n1, n2, d, eps, miter, (double*)ws, plan, pal, iters,
+                       S(stream));
+    const hipError_t le = hipGetLastError();
+    HIPCHK(hipFreeAsync(ws, S(stream)));
+    if (le != hipSuccess) return fail(AST_E_HIP, std::string("k_ot_admm_big: ") + hipGetErrorString(le));
     return 0;
 }
 

@@ -347,7 +347,12 @@ void launch_adam_dev(float* x, float* m, float* v, const float* g, size_t n, int
 
 // batched ADMM optimal transport between palettes (ot_admm.hip, optimal_transport.py:77-162)
 size_t ot_lds_bytes(int n1, int n2);
-int ot_max_cells();
+int ot_max_cells();   // register kernel limit; larger problems run k_ot_admm_big
+size_t ot_big_lds_bytes(int n1, int n2);
+size_t ot_big_ws_bytes(int n1, int n2);   // per problem
+void launch_ot_admm_big(const double* p_mod, const double* p_ref, int nprob, int n1, int n2, int d,
+                        double eps, double miter, double* ws, double* plan, double* pal, int* iters,
+                        hipStream_t s);
 void launch_ot_admm(const double* p_mod, const double* p_ref, int nprob, int n1, int n2, int d,
                     double eps, double miter, double* plan, double* pal, int* iters, hipStream_t s);
 

@@ -199,7 +199,157 @@ __global__ void __launch_bounds__(OT_T) k_ot_admm(const double* __restrict__ p_m
     }
 }
 
+// Problems past the register kernel's n1 n2 <= 4096 cells: the same ADMM with every n1 x n2
+// iterate (Sol, Old, Aux[3], Lambda[3]) and the cost matrix in a device workspace of 10 N
+// doubles per problem (L2-resident for palettes of a few thousand cells), one 1024-thread
+// workgroup per problem, cell e = tid + 1024 k; row / column corrections and the reductions in
+// LDS.  The same fp64 operations in the same order per cell; row and column sums in index order.
+constexpr int OTB_T = 1024;
+constexpr int OTB_W = OTB_T / 64;
+
+__global__ void __launch_bounds__(OTB_T) k_ot_admm_big(const double* __restrict__ p_mod,
+                                                       const double* __restrict__ p_ref, int n1,
+                                                       int n2, int d, double eps, double miter,
+                                                       double* __restrict__ ws,
+                                                       double* __restrict__ plan,
+                                                       double* __restrict__ pal, int* __restrict__ iters) {
+    extern __shared__ double lds[];
+    const int N = n1 * n2;
+    double* rc = lds;              // [n1]
+    double* cc = rc + n1;          // [n2]
+    double* redA = cc + n2;        // [OTB_W]
+    double* redB = redA + OTB_W;   // [OTB_W][5]
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const size_t pb = blockIdx.x;
+    const double* P1 = p_mod + pb * n1 * d;
+    const double* P2 = p_ref + pb * n2 * d;
+    double* CM = ws + pb * 10 * (size_t)N;
+    double* SOL = CM + N;
+    double* OLD = SOL + N;
+    double* AX[3] = {OLD + N, OLD + 2 * (size_t)N, OLD + 3 * (size_t)N};
+    double* LM[3] = {OLD + 4 * (size_t)N, OLD + 5 * (size_t)N, OLD + 6 * (size_t)N};
+
+    double cmax = 0.0;
+    for (int e = tid; e < N; e += OTB_T) {
+        const int i = e / n2, j = e - i * n2;
+        double v = 0.0;
+        for (int f = 0; f < d; ++f) {
+            const double df = P1[(size_t)i * d + f] - P2[(size_t)j * d + f];
+            v = v + df * df;
+        }
+        v = sqrt(v);
+        cmax = fmax(cmax, v);
+        CM[e] = v;
+        SOL[e] = OLD[e] = 0.0;
+        for (int q = 0; q < 3; ++q) AX[q][e] = LM[q][e] = 0.0;
+    }
+    cmax = wave_max(cmax);
+    if (lane == 0) redA[w] = cmax;
+    __syncthreads();
+    cmax = redA[0];
+    for (int i = 1; i < OTB_W; ++i) cmax = fmax(cmax, redA[i]);
+    for (int e = tid; e < N; e += OTB_T) CM[e] = CM[e] / cmax;
+    __syncthreads();
+
+    const double hi1 = 1.0 / (double)n1, hi2 = 1.0 / (double)n2;
+    const double fN = (double)N;
+    int it = 0;
+    for (;;) {
+        double t2 = 0.0;
+        for (int e = tid; e < N; e += OTB_T) {
+            const double sa = (AX[0][e] + AX[1][e]) + AX[2][e];
+            const double sl = (LM[0][e] + LM[1][e]) + LM[2][e];
+            double s = ((-CM[e] + RHO * sa) + sl) / (3.0 * RHO);
+            s = s < 0.0 ? 0.0 : s;
+            SOL[e] = s;
+            for (int q = 0; q < 3; ++q) AX[q][e] = s - LM[q][e] / RHO;
+            t2 += AX[2][e];
+        }
+        t2 = wave_sum(t2);
+        if (lane == 0) redA[w] = t2;
+        __syncthreads();   // the block's global writes are visible to the block after the barrier
+        for (int r = tid; r < n1 + n2; r += OTB_T) {
+            double s = 0.0, corr = 0.0;
+            if (r < n1) {
+                for (int j = 0; j < n2; ++j) s += AX[0][r * n2 + j];
+                if (s < 0.0) corr = (0.0 - s) / (double)n2;
+                else if (s > hi1) corr = (hi1 - s) / (double)n2;
+                rc[r] = corr;
+            } else {
+                const int j = r - n1;
+                for (int i = 0; i < n1; ++i) s += AX[1][i * n2 + j];
+                if (s < 0.0) corr = (0.0 - s) / (double)n1;
+                else if (s > hi2) corr = (hi2 - s) / (double)n1;
+                cc[j] = corr;
+            }
+        }
+        double tot = 0.0;
+        for (int i = 0; i < OTB_W; ++i) tot += redA[i];
+        const double corr2 = (1.0 - tot) / fN;
+        __syncthreads();
+        double nr[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int e = tid; e < N; e += OTB_T) {
+            const int i = e / n2, j = e - i * n2;
+            const double s = SOL[e];
+            double ax[3] = {AX[0][e] + rc[i], AX[1][e] + cc[j], AX[2][e] + corr2};
+            for (int q = 0; q < 3; ++q) {
+                AX[q][e] = ax[q];
+                LM[q][e] += RHO * (ax[q] - s);
+            }
+            const double o = OLD[e];
+            nr[0] += (s - o) * (s - o);
+            nr[1] += (s - ax[0]) * (s - ax[0]);
+            nr[2] += (s - ax[1]) * (s - ax[1]);
+            nr[3] += (s - ax[2]) * (s - ax[2]);
+            nr[4] += s * s;
+        }
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            nr[q] = wave_sum(nr[q]);
+            if (lane == 0) redB[w * 5 + q] = nr[q];
+        }
+        __syncthreads();
+        double nt[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int i = 0; i < OTB_W; ++i)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) nt[q] += redB[i * 5 + q];
+        __syncthreads();   // redA / redB / rc / cc are rewritten next iteration
+        if ((double)it > miter) break;
+        const double lim = eps * sqrt(nt[4]);
+        if (sqrt(nt[0]) < lim && sqrt(nt[1]) < lim && sqrt(nt[2]) < lim && sqrt(nt[3]) < lim) break;
+        for (int e = tid; e < N; e += OTB_T) OLD[e] = SOL[e];
+        ++it;
+    }
+    for (int e = tid; e < N; e += OTB_T) plan[pb * N + e] = SOL[e];
+    if (iters && tid == 0) iters[pb] = it;
+    if (!pal) return;
+    __syncthreads();
+    for (int o = tid; o < n1 * d; o += OTB_T) {
+        const int i = o / d, f = o - i * d;
+        double num = 0.0, den = 0.0;
+        for (int j = 0; j < n2; ++j) {
+            num += SOL[i * n2 + j] * P2[(size_t)j * d + f];
+            den += SOL[i * n2 + j];
+        }
+        pal[pb * n1 * d + o] = num / (den + 1e-10);
+    }
+}
+
 }  // namespace
+
+size_t ot_big_lds_bytes(int n1, int n2) {
+    return sizeof(double) * ((size_t)n1 + n2 + OTB_W + 5 * OTB_W);
+}
+size_t ot_big_ws_bytes(int n1, int n2) { return sizeof(double) * 10 * (size_t)n1 * n2; }
+
+void launch_ot_admm_big(const double* p_mod, const double* p_ref, int nprob, int n1, int n2, int d,
+                        double eps, double miter, double* ws, double* plan, double* pal, int* iters,
+                        hipStream_t s) {
+    (void)hipFuncSetAttribute((const void*)k_ot_admm_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)ot_big_lds_bytes(n1, n2));
+    hipLaunchKernelGGL(k_ot_admm_big, dim3(nprob), dim3(OTB_T), ot_big_lds_bytes(n1, n2), s, p_mod,
+                       p_ref, n1, n2, d, eps, miter, ws, plan, pal, iters);
+}
 
 size_t ot_lds_bytes(int n1, int n2) {
     return sizeof(double) * (3 * (size_t)n1 * n2 + n1 + n2 + OT_W + 5 * OT_W);

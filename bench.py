@@ -297,12 +297,28 @@ def cpu_baseline(T, budget_s, gatys=False):
                     'config1_iters_per_s on the same cores'}
 
 
-def block_roofline(precision, B, T, fwd_ms, bwd_ms, traffic):
-    """Roofline of the block kernels, one fwd and one bwd launch (all clips).  Algorithmic
-    bytes: fwd reads e_l and writes e_{l+1} (2A), bwd reads the chain and D_l and
-    writes the chain (3A), A = B T 128 x element size; plus the relu-mask words (16 B per row
-    written by the fwd, 32 B read by the bwd).  FLOP: 131072 per row (2 (384 + 128) 128); the
-    split mode executes three MFMA products per FLOP."""
+def lib_sha16():
+    """sha256 (16 hex) of the libastyle.so this process loads: ties profiles/traffic.json's PMC
+    bytes to the binary they were measured on."""
+    import hashlib
+    from audio_style_transfer_amd import _lib
+    try:
+        with open(_lib.LIB_PATH, 'rb') as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def block_roofline(precision, B, T, fwd_ms, bwd_ms, traffic, ms_per_step, gram_ms, L=30,
+                   nblk=30):
+    """Roofline of the block kernels.  Per launch (all B clips): algorithmic bytes
+    fwd = read e_l + write e_{l+1} (2A) + the relu-mask words (16 B per row written, 16 B of
+    the previous layer's read); bwd = read the chain and D_l, write the chain (3A) + 32 B of
+    mask words per row; A = B T 128 x element size.  FLOP = 131072 per row (2 (384 + 128) 128);
+    the split mode executes three MFMA products per FLOP.  Each kernel's binding fraction is
+    the larger of its HBM and executed-MFMA fractions.  The top-level object is the dominant
+    kernel (the one with more time per step); 'step' is the step-level HBM fraction:
+    algorithmic bytes of the blocks and the Gram per step / ms_per_step / 8 TB/s."""
     esz = 2.0 if precision == 'bf16' else 4.0
     rows = float(B) * T
     A = rows * 128 * esz
@@ -311,31 +327,38 @@ def block_roofline(precision, B, T, fwd_ms, bwd_ms, traffic):
     flops = 131072.0 * rows
     mult = 3.0 if precision == 'split' else 1.0
     peak = FP32_MFMA_PEAK_TFLOPS if precision == 'fp32' else F16_MFMA_PEAK_TFLOPS
+    tf = traffic or {}
 
-    def one(ms, nbytes, tb):
+    def one(name, ms, nbytes, tb):
         mf = flops * mult / (ms * 1e-3) / 1e12
         gb = nbytes / (ms * 1e-3) / 1e9
-        d = {'launch_ms': ms, 'algorithmic_bytes': nbytes, 'algorithmic_flops': flops,
-             'executed_mfma_flops': flops * mult, 'mfma_TFLOPs': mf, 'mfma_frac': mf / peak,
-             'hbm_GBs': gb, 'hbm_frac': gb / HBM_PEAK_GBS, 'traffic': tb}
-        d['bound'] = 'mfma' if d['mfma_frac'] >= d['hbm_frac'] else 'hbm'
+        d = {'kernel': name, 'launch_ms': ms, 'algorithmic_bytes': nbytes,
+             'algorithmic_flops': flops, 'executed_mfma_flops': flops * mult, 'mfma_TFLOPs': mf,
+             'mfma_frac': mf / peak, 'hbm_GBs': gb, 'hbm_frac': gb / HBM_PEAK_GBS, 'traffic': tb}
+        if d['mfma_frac'] >= d['hbm_frac']:
+            d.update(bound='mfma', achieved=mf, peak=peak, unit='TFLOP/s', frac=d['mfma_frac'])
+        else:
+            d.update(bound='hbm', achieved=gb, peak=HBM_PEAK_GBS, unit='GB/s', frac=d['hbm_frac'])
         return d
 
-    tf = traffic or {}
-    f = one(fwd_ms, fbytes, tf.get('fwd'))
-    b = one(bwd_ms, bbytes, tf.get('bwd'))
-    bound = 'mfma' if (f['mfma_frac'] + b['mfma_frac']) >= (f['hbm_frac'] + b['hbm_frac']) else 'hbm'
-    if bound == 'mfma':
-        roof = {'bound': 'mfma', 'achieved': (f['mfma_TFLOPs'] + b['mfma_TFLOPs']) / 2, 'peak': peak,
-                'unit': 'TFLOP/s'}
-    else:
-        roof = {'bound': 'hbm', 'achieved': (f['hbm_GBs'] + b['hbm_GBs']) / 2, 'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s'}
-    roof['frac'] = roof['achieved'] / roof['peak']
-    roof['traffic'] = ((tf['fwd'] + tf['bwd']) / 2) if tf.get('fwd') and tf.get('bwd') else None
-    roof.update({'kernel': 'k_block_fwd*/k_block_bwd* (fused dilated conv + 1x1 + epilogues), '
-                           'mean of one fwd and one bwd launch; fwd / bwd below',
-                 'fwd': f, 'bwd': b})
+    suffix = {'split': '_s', 'bf16': '_c', 'fp32': ''}[precision]
+    f = one('k_block_fwd' + suffix, fwd_ms, fbytes, tf.get('fwd'))
+    b = one('k_block_bwd' + suffix, bwd_ms, bbytes, tf.get('bwd'))
+    dom = b if bwd_ms >= fwd_ms else f
+    roof = {k: dom[k] for k in ('bound', 'achieved', 'peak', 'unit', 'frac', 'traffic', 'kernel')}
+    roof['note'] = ('dominant kernel (%.1f of %.1f ms/step in the blocks); achieved = algorithmic '
+                    'bytes (or executed MFMA flops) per launch / its HIP-event launch time; traffic = '
+                    'PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, profiles/traffic.json, '
+                    'null unless measured on this libastyle.so)' % (nblk * dom['launch_ms'],
+                                                                      nblk * (fwd_ms + bwd_ms)))
+    step_bytes = nblk * (fbytes + bbytes) + 3 * L * A
+    roof['fwd'] = f
+    roof['bwd'] = b
+    roof['step'] = {'algorithmic_bytes': step_bytes, 'ms': ms_per_step,
+                    'achieved_GBs': step_bytes / (ms_per_step * 1e-3) / 1e9,
+                    'frac': step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    'note': '%d block fwd + bwd launches and the Gram (fwd reads L A, bwd reads '
+                            'L A and writes L A, L = %d) per step' % (nblk, L)}
     return roof
 
 
@@ -375,11 +398,15 @@ def rank_main(args):
     fwd_ms = tm['block_fwd_ms'] / (calls * nblk)
     bwd_ms = tm['block_bwd_ms'] / (calls * nblk)
     traffic = None
+    sha = lib_sha16()
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get('precision') == args.precision and tj.get('clips') == B and tj.get('T') == T:
-            traffic = {'fwd': tj['fwd_bytes_per_launch'], 'bwd': tj['bwd_bytes_per_launch']}
+        if (tj.get('precision') == args.precision and tj.get('clips') == B and tj.get('T') == T
+                and tj.get('gatys', False) == args.gatys and tj.get('lib_sha16') == sha):
+            traffic = {'fwd': tj['fwd_bytes_per_launch'], 'bwd': tj['bwd_bytes_per_launch'],
+                       'gram_fwd': tj.get('gram_fwd_bytes_per_launch'),
+                       'gram_bwd': tj.get('gram_bwd_bytes_per_launch'), 'source': tj.get('source')}
     except Exception:
         traffic = None
     gram_fwd_ms = tm['gram_fwd_ms'] / calls
@@ -399,14 +426,20 @@ def rank_main(args):
                    'precision': args.precision, 'precision_detail': PREC_NOTE[args.precision],
                    'hip_graph': bool(args.graph)},
         'clip_iters_per_s': value * 256.0,
-        'roofline': block_roofline(args.precision, B, T, fwd_ms, bwd_ms, traffic),
+        'roofline': block_roofline(args.precision, B, T, fwd_ms, bwd_ms, traffic,
+                                   el / args.steps * 1e3, gram_fwd_ms + gram_bwd_ms),
+        'lib_sha16': sha,
         'kernels_ms_per_step': {'block_fwd': tm['block_fwd_ms'] / calls,
                                 'block_bwd': tm['block_bwd_ms'] / calls,
                                 'gram_fwd': gram_fwd_ms, 'gram_bwd': gram_bwd_ms,
                                 'other': tm['other_ms'] / calls},
         'gram_roofline': {'bound': 'hbm', 'fwd_achieved_GBs': gbytes / (gram_fwd_ms * 1e-3) / 1e9,
                           'bwd_achieved_GBs': 2 * gbytes / (gram_bwd_ms * 1e-3) / 1e9,
-                          'peak': HBM_PEAK_GBS},
+                          'fwd_frac': gbytes / (gram_fwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                          'bwd_frac': 2 * gbytes / (gram_bwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                          'peak': HBM_PEAK_GBS,
+                          'fwd_traffic': (traffic or {}).get('gram_fwd'),
+                          'bwd_traffic': (traffic or {}).get('gram_bwd')},
         'loss_first_last': [first_loss, last_loss],
         'nonfinite_clips': bad,
     }

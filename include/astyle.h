@@ -178,7 +178,10 @@ int ast_restore(ast_ctx* ctx, const char* prefix);
  * p_mod_dev [n1, d] and p_ref_dev [n2, d] float64 -> plan_dev [n1, n2] (the transport plan),
  * palette_dev [n1, d] (p_ref moved onto p_mod's palette: plan p_ref / (row sums + 1e-10);
  * NULL = skip), iters_dev [nprob] int (ADMM iterations; NULL = skip).  eps, miter as OT_ADMM's
- * (1e-4, 1e5).  Needs n1 n2 <= 4096.  fp64, one workgroup per problem; no context. */
+ * (1e-4, 1e5).  fp64, one workgroup per problem; no context.  n1 n2 <= 4096: iterates in
+ * registers; larger (up to n1 n2 <= 2^26, n1 + n2 <= 20000): iterates in a device workspace
+ * the call allocates and frees stream-ordered (hipMallocAsync), so that form is not for
+ * capture in a graph that outlives the call. */
 int ast_ot_admm(const double* p_mod_dev, const double* p_ref_dev, int nprob, int n1, int n2, int d,
                 double eps, double miter, double* plan_dev, double* palette_dev, int* iters_dev,
                 void* stream);

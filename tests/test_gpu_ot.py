@@ -53,11 +53,11 @@ def test_ot_batch_invariance_and_limits():
         assert torch.equal(p1[0], plans[k]) and torch.equal(q1[0], pals[k]) and int(i1[0]) == int(its[k])
     po, _ = O.ot_admm(a[150], b[150])
     assert rel(plans[150].cpu().numpy(), po) <= 1e-3
-    # largest problem: 64 x 64 cells
+    # largest register-kernel problem: 64 x 64 cells
     p, _, it = OT.ot_admm_batched(r.rand(1, 64, 8), r.rand(1, 64, 8), miter=300)
     assert int(it[0]) <= 301 and torch.isfinite(p).all()
-    with pytest.raises(AstError):
-        OT.ot_admm_batched(r.rand(1, 65, 4), r.rand(1, 64, 4))
+    with pytest.raises(AstError):        # n1 + n2 past the LDS row / column correction space
+        OT.ot_admm_batched(r.rand(1, 15000, 1), r.rand(1, 6000, 1))
     p0, _, _ = OT.ot_admm_batched(np.zeros((0, 3, 4)), np.zeros((0, 5, 4)))
     assert p0.shape == (0, 3, 5)
 
@@ -74,3 +74,22 @@ def test_ot_helpers_match_oracle():
     assert rel(OT.projection_sum_equal(x, 1.0), O.project_total(x, 1.0)) <= 1e-15
     plan, _ = O.ot_admm(w1, w2)
     assert rel(OT.transform_palette(w1, w2, plan), O.transform_palette(w1, w2, plan)) <= 1e-14
+
+
+@pytest.mark.parametrize('n1,n2,d,seed', [(65, 64, 4, 9), (80, 80, 16, 8), (100, 70, 8, 10)])
+def test_ot_admm_large_palettes(n1, n2, d, seed):
+    """Past the register kernel's n1 n2 <= 4096: the device-workspace kernel (k_ot_admm_big),
+    same iteration count as the oracle (or one apart) and the plan to round-off; two problems
+    in one call are each what a single call gives."""
+    from audio_style_transfer_amd import optimal_transport as OT
+    r = np.random.RandomState(seed)
+    w1, w2 = r.rand(n1, d), r.rand(n2, d)
+    plan_o, it_o = O.ot_admm(w1, w2)
+    plan, pal, its = OT.ot_admm_batched(np.stack([w1, w1[::-1].copy()]), np.stack([w2, w2]))
+    p0, q0, it = plan[0].cpu().numpy(), pal[0].cpu().numpy(), int(its[0])
+    print('%dx%d d=%d: iterations hip %d oracle %d, plan rel-L2 %.2e' % (n1, n2, d, it, it_o, rel(p0, plan_o)))
+    assert abs(it - it_o) <= 1
+    assert rel(p0, plan_o) <= (1e-9 if it == it_o else 1e-3)
+    assert rel(q0, O.transform_palette(w1, w2, plan_o)) <= (1e-9 if it == it_o else 1e-3)
+    p1, _, i1 = OT.ot_admm_batched(w1[::-1].copy()[None], w2[None])
+    assert torch.equal(p1[0], plan[1]) and int(i1[0]) == int(its[1])

@@ -76,11 +76,20 @@ def main(tag, precision, clips, T):
                                             for k in ks) / n,
                 'avg_ms': sum(stats[k]['avg_ms'] * stats[k]['calls'] for k in ks) / n, 'calls': n}
     fw, bw = pick('k_block_fwd'), pick('k_block_bwd')
+    gatys = any('k_gatys' in k for k in stats)
+    gf, gb = (pick('k_gatys_fwd'), pick('k_gatys_bwd')) if gatys else (pick('k_gram_fwd'), pick('k_gram_bwd'))
     if 'hbm_bytes_per_launch' in fw and 'hbm_bytes_per_launch' in bw:
-        tj = {'precision': precision, 'clips': clips, 'T': T, 'source': tag,
-              'block_bytes_per_launch': (fw['hbm_bytes_per_launch'] + bw['hbm_bytes_per_launch']) / 2,
+        # the library the profiled runs loaded (tools/profile.sh records its sha256)
+        with open(os.path.join(src, 'lib.sha256')) as f:
+            sha = f.read().split()[0][:16]
+        tj = {'precision': precision, 'clips': clips, 'T': T, 'gatys': gatys, 'source': tag,
+              'lib_sha16': sha,
               'fwd_bytes_per_launch': fw['hbm_bytes_per_launch'],
-              'bwd_bytes_per_launch': bw['hbm_bytes_per_launch']}
+              'bwd_bytes_per_launch': bw['hbm_bytes_per_launch'],
+              'fwd_ms': fw['avg_ms'], 'bwd_ms': bw['avg_ms'],
+              'gram_fwd_bytes_per_launch': gf.get('hbm_bytes_per_launch'),
+              'gram_bwd_bytes_per_launch': gb.get('hbm_bytes_per_launch'),
+              'gram_fwd_ms': gf.get('avg_ms'), 'gram_bwd_ms': gb.get('avg_ms')}
         with open(os.path.join(dst, 'traffic.json'), 'w') as f:
             json.dump(tj, f, indent=1)
     for k, v in sorted(stats.items(), key=lambda kv: -kv[1]['total_ms'])[:10]:
