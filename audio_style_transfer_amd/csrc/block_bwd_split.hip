@@ -112,11 +112,12 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         if (HAS_D) { e.x += lg[k].x; e.y += lg[k].y; e.z += lg[k].z; e.w += lg[k].w; }
         *reinterpret_cast<float4*>(er + ru.ero + 8 * k * RS) = e;
         const float sk = (zb >> k) & 1u ? 0.f : s;
-        uint2 hi, lo;
-        split4(v.x * sk, v.y * sk, v.z * sk, v.w * sk, hi, lo);
+        uint32_t h01, l01, h23, l23;
+        split2s(v.x * sk, v.y * sk, h01, l01);
+        split2s(v.z * sk, v.w * sk, h23, l23);
         uint8_t* p = XS + ru.imgo + 8 * k * RS;
-        *reinterpret_cast<uint2*>(p) = hi;
-        *reinterpret_cast<uint2*>(p + 256) = lo;
+        *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
+        *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
     };
     // ---- relu-mask words (u16, position-indexed): u > 0 of the tile's columns and halos,
     //      e_l > 0 of its columns ----
@@ -175,11 +176,12 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         } else {
             // the scale after the mask (f is a power of two: the same values), so that the
             // split's low half fuses with it into one v_fma_mix_f32
-            uint2 hi, lo;
-            split4(gq.x * f, gq.y * f, gq.z * f, gq.w * f, hi, lo);
+            uint32_t h01, l01, h23, l23;
+            split2s(gq.x * f, gq.y * f, h01, l01);
+            split2s(gq.z * f, gq.w * f, h23, l23);
             uint8_t* p = XG + (J < 2 ? Lv[J] : Lhw) * RS + 2 * (chb + 8 * g);
-            *reinterpret_cast<uint2*>(p) = hi;
-            *reinterpret_cast<uint2*>(p + 256) = lo;
+            *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
+            *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
         }
     };
 

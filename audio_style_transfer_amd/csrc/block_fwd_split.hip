@@ -42,6 +42,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];   // fp32 e_l (residual) rows
     __shared__ __attribute__((aligned(16))) uint8_t XV[TMS * RS];   // split v image
     __shared__ __attribute__((aligned(16))) float BIAS[2 * C];      // b_d, b_r
+    __shared__ __attribute__((aligned(16))) float BDS[C];           // b_d 2^m_v (the current clip's v scale)
     __shared__ __attribute__((aligned(16))) uint16_t MBU[TMS * 8];  // u > 0 words of the tile
     __shared__ __attribute__((aligned(16))) uint16_t MBE[TMS * 8];  // e_{l+1} > 0 words
     __shared__ int MBT[TMS];                                        // time of each tile column
@@ -138,11 +139,12 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         const float sk = (zb >> k) & 1u ? 0.f : s;
         v.x = __int_as_float(max(__float_as_int(v.x), 0)); v.y = __int_as_float(max(__float_as_int(v.y), 0));
         v.z = __int_as_float(max(__float_as_int(v.z), 0)); v.w = __int_as_float(max(__float_as_int(v.w), 0));
-        uint2 hi, lo;
-        split4(v.x * sk, v.y * sk, v.z * sk, v.w * sk, hi, lo);
+        uint32_t h01, l01, h23, l23;
+        split2(v.x * sk, v.y * sk, h01, l01);
+        split2(v.z * sk, v.w * sk, h23, l23);
         uint8_t* p = IMG + imgo + 8 * k * RS;
-        *reinterpret_cast<uint2*>(p) = hi;
-        *reinterpret_cast<uint2*>(p + 256) = lo;
+        *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
+        *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
     };
 
     // e_{l+1} > 0 words of a finished tile -> next layer's positions (wave w: columns 16 w..)
@@ -219,29 +221,41 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     };
 
     // ---- epilogue 1 of column half j, unit g in two parts: u, bits; v -> split v image ----
+    // v = relu(u) 2^m_v = relu(acc 2^(m_v - m_e - k_d) + b_d 2^m_v): the scale folded into the fma
+    // (powers of two: the same values); the u > 0 bits from the split's rtz hi halves (splitwave.h
+    // nz2; SW_UBITS_EXACT: from v itself)
     f32x16 acc1[2];
-    float inv1 = 0.f, sv = 0.f;
+    float a1 = 0.f;
+    float bs_sv = -1.f;   // the v scale BDS holds
     uint32_t mu_w = 0;
-    float4 e1u;
+    float4 e1v;
     auto epi1_part = [&](int j, int g, int part) {
         if (part == 0) {
-            const float4 b4 = *reinterpret_cast<const float4*>(&BIAS[chb + 8 * g]);
-            e1u.x = fmaf(acc1[j][4 * g + 0], inv1, b4.x);
-            e1u.y = fmaf(acc1[j][4 * g + 1], inv1, b4.y);
-            e1u.z = fmaf(acc1[j][4 * g + 2], inv1, b4.z);
-            e1u.w = fmaf(acc1[j][4 * g + 3], inv1, b4.w);
-            mu_w = or_pos_bits4(mu_w, e1u.x, e1u.y, e1u.z, e1u.w, g);
+            const float4 b4 = *reinterpret_cast<const float4*>(&BDS[chb + 8 * g]);
+            e1v.x = fmaxf(fmaf(acc1[j][4 * g + 0], a1, b4.x), 0.f);
+            e1v.y = fmaxf(fmaf(acc1[j][4 * g + 1], a1, b4.y), 0.f);
+            e1v.z = fmaxf(fmaf(acc1[j][4 * g + 2], a1, b4.z), 0.f);
+            e1v.w = fmaxf(fmaf(acc1[j][4 * g + 3], a1, b4.w), 0.f);
         } else {
-            uint2 hi, lo;
-            split4(fmaxf(e1u.x, 0.f) * sv, fmaxf(e1u.y, 0.f) * sv, fmaxf(e1u.z, 0.f) * sv,
-                   fmaxf(e1u.w, 0.f) * sv, hi, lo);
+            uint32_t h01, l01, h23, l23;
+            split2(e1v.x, e1v.y, h01, l01);
+            split2(e1v.z, e1v.w, h23, l23);
             uint8_t* p = XV + (32 * j + r) * RS + 2 * (chb + 8 * g);
-            *reinterpret_cast<uint2*>(p) = hi;
-            *reinterpret_cast<uint2*>(p + 256) = lo;
+            *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
+            *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
+#ifdef SW_UBITS_EXACT
+            mu_w = or_pos_bits4(mu_w, e1v.x, e1v.y, e1v.z, e1v.w, g);
             if (g == 3) {
                 MBU[(32 * j + r) * 8 + 4 * h + w] = (uint16_t)mu_w;
                 mu_w = 0;
             }
+#else
+            mu_w = or_bits4(mu_w, h01, h23, g);
+            if (g == 3) {
+                MBU[(32 * j + r) * 8 + 4 * h + w] = (uint16_t)mask16(mu_w);
+                mu_w = 0;
+            }
+#endif
         }
     };
 
@@ -343,8 +357,12 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         if (nt.b != cu.b) gm_c = sload(a.gmax_in + nt.b);   // (usually the same clip: tile order)
         const float s_next = exp2i(scale_exp(gm_c));
         const uint32_t zn = zero_bits_of(nt);
-        inv1 = exp2i(-(m_e + a.kd));
-        sv = exp2i(m_v);
+        const float sv = exp2i(m_v);
+        a1 = exp2i(m_v - m_e - a.kd);
+        if (sv != bs_sv) {   // the clip's v scale changed: b_d 2^m_v of this wave's channels (only
+            bs_sv = sv;      // this wave reads them, in program order after these writes)
+            if (lane < 32) BDS[32 * w + lane] = BIAS[32 * w + lane] * sv;
+        }
         uint8_t* erp = &ER[(it & 1) ^ 1][0];   // the previous tile's residual, then the next's
 
         STAMP(10)
