@@ -34,11 +34,16 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 // Diagnostic phase stamps (guide: In-kernel stamps).  Only -DASTYLE_STAMPS builds execute
-// them; cycle deltas per phase are summed per wave and added to a.stamps[phase] at exit.
+// them; cycle deltas per phase are summed per wave and added to a.stamps[phase] at exit.  Slot
+// 15 takes the wave's lifetime in s_memrealtime ticks (100 MHz): shader cycles / ticks x 100 MHz
+// is the clock the kernel actually ran at.
 #ifdef ASTYLE_STAMPS
-#define STAMP_DECL unsigned long long st_acc[16] = {}; unsigned long long st_prev = stamp_now();
+#define STAMP_DECL unsigned long long st_acc[16] = {}; unsigned long long st_prev = stamp_now(); \
+    const unsigned long long st_rt0 = __builtin_amdgcn_s_memrealtime();
 #define STAMP(k) { const unsigned long long st_t = stamp_now(); st_acc[k] += st_t - st_prev; st_prev = st_t; }
-#define STAMP_FLUSH(ptr) if (((threadIdx.x & 63) == 0) && (ptr)) { for (int k = 0; k < 16; ++k) atomicAdd(&(ptr)[k], st_acc[k]); }
+#define STAMP_FLUSH(ptr) if (((threadIdx.x & 63) == 0) && (ptr)) { \
+    st_acc[15] = __builtin_amdgcn_s_memrealtime() - st_rt0; \
+    for (int k = 0; k < 16; ++k) atomicAdd(&(ptr)[k], st_acc[k]); }
 __device__ __forceinline__ unsigned long long stamp_now() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);

@@ -6,7 +6,7 @@ scipy L-BFGS-B minimize(maxiter=100) whose every function evaluation is one ast_
 (ScipyOptimizerInterface, methods.py:132-137,167), early stop when an epoch used < 50
 evaluations (methods.py:180), the four loss scalars of every evaluation written to a TF event
 file in the log dir (methods.py:127-130,156; summary.EventWriter).  Additions: --optimizer
-device (the same L-BFGS-B on the GPU), --precision split|bf16, --weights (npz of TF-named
+device (the same L-BFGS-B on the GPU), --precision split (default) | fp32 | bf16, --weights (npz of TF-named
 encoder variables), --resume (continue after the last finished epoch: each epoch's end point
 is saved as <savepath>/state.npz; an epoch is a fresh minimize call, so x is the whole state).
 
@@ -26,7 +26,7 @@ import warnings
 import numpy as np
 import torch
 
-from . import checkpoint, summary, utils
+from . import _lib, checkpoint, summary, utils
 from .engine import StyleEngine, resolve_style_ids
 from .weights import synthetic_weights
 
@@ -58,7 +58,7 @@ class GatysNet(object):
                  checkpoint_path='./nsynth/model/wavenet-ckpt/model.ckpt-200000',
                  logdir='./log', figdir='./data/fig', stack=0, batch_size=16384, sr=16000,
                  cont_lyr_ids=[29], nb_channels=128, cnt_channels=128, gatys=False,
-                 style_lyr_ids=None, precision='fp32', device=None, weights=None, plots=True,
+                 style_lyr_ids=None, precision='split', device=None, weights=None, plots=True,
                  optimizer='scipy'):
         self.logdir = logdir
         self.savepath = savepath
@@ -173,8 +173,12 @@ class GatysNet(object):
                                 'loss/regularizer': p[3], 'loss/main_loss': p[0]}, step)
 
         def fg(v):
+            nonlocal eng
             xd.copy_(torch.from_numpy(v.astype(np.float32)).view(1, T))
             parts, grad = eng.loss_grad(xd)                               # incl. gamma * reg
+            if eng.precision == 'split' and self._split_out_of_range(eng, log):
+                eng = self._fp32_engine(phi_c, phi_s, lambd, gamma)
+                parts, grad = eng.loss_grad(xd)
             p = parts[0].cpu().numpy().astype(np.float64)
             loss, reg = float(p[0]), float(p[3])
             history.append((loss, float(p[1]), float(p[2]), reg))
@@ -198,6 +202,11 @@ class GatysNet(object):
             else:
                 info = loop.minimize(torch.tensor(x[None], dtype=torch.float64)
                                      if ep == start_ep else None)
+                if eng.precision == 'split' and self._split_out_of_range(eng, log):
+                    # redo the epoch from its start point x with the fp32 kernels
+                    eng = self._fp32_engine(phi_c, phi_s, lambd, gamma)
+                    loop = LbfgsLoop(eng, maxiter=maxiter)
+                    info = loop.minimize(torch.tensor(x[None], dtype=torch.float64))
                 x = loop.state(with_x=True)[1][0].cpu().numpy()
                 state['i'] = int(info[0, 2])
                 p = loop.parts[0].cpu().numpy().astype(np.float64)
@@ -221,6 +230,30 @@ class GatysNet(object):
         writer.close()
         self.history = history
         return x
+
+    def _split_out_of_range(self, eng, log) -> bool:
+        """After a split-precision evaluation: AST_RANGE_* flags of the clip (engine.range_flags).
+        Non-finite results or operands outside the split-fp16 range (flags 1, 2, 4) -> True (the
+        caller switches to the fp32 kernels); operands below 2^-60 (8) only lose low-order bits
+        and are reported once."""
+        f = int(eng.range_flags().max().item())
+        bad = f & (_lib.RANGE_NONFINITE | _lib.RANGE_ACT | _lib.RANGE_GRAD)
+        if f & _lib.RANGE_TINY and not getattr(self, '_tiny_warned', False):
+            self._tiny_warned = True
+            warnings.warn('split precision: operands below 2^-60 in this clip (low-order bits '
+                          'lost; --precision fp32 keeps them)')
+        if bad:
+            log('split precision: range flags %d for this clip; switching to --precision fp32' % f)
+        return bool(bad)
+
+    def _fp32_engine(self, phi_c, phi_s, lambd, gamma):
+        self.precision = 'fp32'
+        new = self.build(self.batch_size, lambd=lambd)
+        new.set_targets(torch.as_tensor(phi_c, dtype=torch.float32),
+                        torch.as_tensor(phi_s, dtype=torch.float32))
+        new.set_gamma(gamma)
+        self.engine = new
+        return new
 
     def _run_fingerprint(self, phi_c, phi_s, lambd, gamma, optimizer):
         """What a saved epoch state depends on: the targets (hence the content / style files and
@@ -307,9 +340,11 @@ def make_parser():
     parser.add_argument('--outdir', help='path to output', nargs='?', default='./data/out')
     parser.add_argument('--logdir', help='path to logs', nargs='?', default='./log')
     parser.add_argument('--cmt')
-    parser.add_argument('--precision', default='fp32', choices=['fp32', 'split', 'bf16'],
-                        help='fp32: reference numerics; split: fp32 storage, split-fp16/bf16 '
-                             'MFMA (fp32-accurate, faster); bf16: bf16 storage + bf16 MFMA')
+    parser.add_argument('--precision', default='split', choices=['fp32', 'split', 'bf16'],
+                        help='split (default): fp32 storage, split-fp16 MFMA with fp32 '
+                             'accumulation (gradient within 2e-4 rel-L2 of fp64, range-checked '
+                             'per clip: ast_range_flags); fp32: plain fp32 FMA kernels; bf16: '
+                             'bf16 storage + bf16 MFMA')
     parser.add_argument('--weights', default=None, help='npz of TF-named encoder weights')
     parser.add_argument('--no_plots', action='store_true', help='skip the Gram PNGs')
     parser.add_argument('--optimizer', default='scipy', choices=['scipy', 'device'],

@@ -39,7 +39,7 @@ def test_cli_parses_readme_example():
     a = methods.make_parser().parse_args(
         'pachelbel organ --epochs 100 --cont_lyrs 25 --stack 0 --lambd 100 --gamma 0'.split())
     assert a.cont_lyrs == [25] and a.stack == 0 and a.lambd == 100.0 and a.gamma == 0.0
-    assert a.batch_size == 16384 and a.gatys is False and a.precision == 'fp32'
+    assert a.batch_size == 16384 and a.gatys is False and a.precision == 'split'
     assert methods.make_parser().parse_args(['a', 'b', '--gatys']).gatys is True
 
 
@@ -48,6 +48,30 @@ def test_output_dir_ignores_added_flags(tmp_path):
     d = methods.get_dir(str(tmp_path), a)
     assert 'precision' not in d and os.path.isdir(d)
     assert os.path.basename(d).startswith('ours__btch_16384_')
+
+
+def test_split_range_guard():
+    """GatysNet._split_out_of_range: AST_RANGE_* flags 1/2/4 of a split evaluation switch the run
+    to the fp32 kernels; 8 (operands below 2^-60) only warns, once."""
+    import torch
+    from audio_style_transfer_amd import _lib
+
+    class Eng:
+        def __init__(self, f):
+            self.f = f
+
+        def range_flags(self):
+            return torch.tensor([0, self.f], dtype=torch.int32)
+
+    net = methods.GatysNet.__new__(methods.GatysNet)
+    logs = []
+    assert not net._split_out_of_range(Eng(0), logs.append)
+    for f in (_lib.RANGE_NONFINITE, _lib.RANGE_ACT, _lib.RANGE_GRAD, _lib.RANGE_ACT | _lib.RANGE_TINY):
+        assert net._split_out_of_range(Eng(f), logs.append)
+    assert len(logs) == 4 and 'fp32' in logs[0]
+    with pytest.warns(UserWarning):
+        net2 = methods.GatysNet.__new__(methods.GatysNet)
+        assert not net2._split_out_of_range(Eng(_lib.RANGE_TINY), logs.append)
 
 
 def test_style_layer_resolution():

@@ -47,6 +47,9 @@ else:
             if v[k]:
                 print('%-48s %6.1f %%   %8.0f cycles/tile/wave' % (names[k], 100.0 * v[k] / tot, v[k] / (4 * 256 * tiles)))
         print('%-48s %8.0f cycles per wave per launch' % ('total', tot / (4 * 256 * 30)))
+    if v[15]:   # wave lifetimes in 100-MHz ticks: the clock the kernels ran at
+        cyc = sum(v[k] for k in range(15))
+        print('%-48s %8.0f MHz (shader cycles / s_memrealtime ticks, all stamped kernels)' % ('effective clock', 100.0 * cyc / v[15]))
     sys.exit(0)
 for lo, hi in groups:
     tot = sum(v[lo:hi])
