@@ -26,6 +26,7 @@
 // floor of 6.2k; moving the loads / conversions between phases does not change the tile time.
 #include "splitwave.h"
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace ast {
@@ -443,7 +444,18 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
 
 }  // namespace
 
+bool launch_block_fwd_roles(const FwdArgsS& a, hipStream_t s);   // block_fwd_roles.hip
+
+// ASTYLE_FWD_ROLES=1 selects the role-split kernel (block_fwd_roles.hip, bit-identical results;
+// measured 3-4 % slower than this one-wave-per-SIMD kernel)
+static bool fwd_roles() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("ASTYLE_FWD_ROLES"); v = e ? (atoi(e) != 0) : 0; }
+    return v != 0;
+}
+
 void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
+    if (fwd_roles()) { launch_block_fwd_roles(a0, s); return; }
     FwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
     a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));

@@ -109,6 +109,20 @@ __device__ __forceinline__ int pos_time(int p, const FDiv& fn, int d) {
     return (p - q * (int)fn.n) * d + q;
 }
 
+// raw buffer access: a uniform base in the resource (scalar registers) + a 32-bit per-lane
+// offset + a uniform offset, so a kernel keeps one VGPR per access stream instead of a 64-bit
+// address per lane (the role-split kernels' residual waves are register-bound)
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t mk_rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float4 bld4(rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bst4(rsrc_t r, uint32_t voff, uint32_t soff, float4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, 0);
+}
+
 __device__ __forceinline__ uint4 lds16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
 // Image rows of a tile with no source row are zeroed at conversion (unmasked layouts): the pad

@@ -33,6 +33,23 @@ if prec == 'bf16':
              'bwd: step 3 (mask, +tot, +D, stores)', '-', '-', '-', '-']
     tiles = B * T // 128 * 30 / 256   # tiles per CU over the 30 block launches
     groups = ((0, 4), (4, 8))
+elif os.environ.get('ASTYLE_FWD_ROLES', '1') != '0' and mode == 'fwd':
+    # role-split forward (block_fwd_roles.hip): 4 dconv + 4 residual waves per CU
+    names = {14: 'dconv: prologue + S_0', 6: 'dconv: GEMM1 half 0', 7: 'dconv: epi1 half 0', 8: 'dconv: GEMM1 half 1',
+             9: 'dconv: epi1 half 1', 10: 'dconv: S wait', 13: 'resid: prologue + S_0', 12: 'resid: convert (period 0)',
+             11: 'resid: top (scales, max flush)', 0: 'resid: res0 + GEMM2 h0 + convert 0..4', 2: 'resid: epi2 h0',
+             3: 'resid: res1 + GEMM2 h1 + convert 5..8', 5: 'resid: epi2 h1', 1: 'resid: mask stores', 4: 'resid: S wait'}
+    tiles = B * T // 64 * 30 / 256
+    for grp in ((14, 6, 7, 8, 9, 10), (13, 12, 11, 0, 2, 3, 5, 1, 4)):
+        tot = sum(v[k] for k in grp)
+        for k in grp:
+            if v[k]:
+                print('%-48s %6.1f %%   %8.0f cycles/tile/wave' % (names[k], 100.0 * v[k] / tot, v[k] / (4 * 256 * tiles)))
+        print('%-48s %8.0f cycles per wave per launch' % ('total', tot / (4 * 256 * 30)))
+    if v[15]:
+        cyc = sum(v[k] for k in range(15))
+        print('%-48s %8.0f MHz (shader cycles / s_memrealtime ticks, all stamped kernels)' % ('effective clock', 100.0 * cyc / v[15]))
+    sys.exit(0)
 else:
     names = {13: 'fwd: prologue (weights, first tile)', 14: 'bwd: prologue (weights, first tile)', 0: 'fwd: T barrier', 10: 'fwd: top (scales, scalar loads)', 5: 'fwd: A GEMM1 half 0 + epi2(prev)',
              1: 'fwd: B GEMM1 half 1 + epi1 half 0 + barrier', 2: 'fwd: C GEMM2 half 0 + epi1 half 1 + barrier',
