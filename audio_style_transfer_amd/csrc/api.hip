@@ -357,6 +357,21 @@ void launch_gram_bwd_any(ast_ctx* x, const GramArgs& g, hipStream_t s) {
     else launch_gram_bwd(g, s);
 }
 
+// The split ours-Gram backward computes the content tap's gradient and squared error itself
+// when there is exactly one content occurrence and its tensor is style-tapped (configs[2]:
+// cont 29): k_content's cg buffer (written, then read back by the Gram backward) is skipped.
+// ASTYLE_FUSE_CONTENT=0 keeps the separate kernel.
+int fused_content_occ(const ast_ctx* x) {
+    static int en = -1;
+    if (en < 0) { const char* e = getenv("ASTYLE_FUSE_CONTENT"); en = e ? (atoi(e) != 0) : 1; }
+    if (!en || !x->split || x->cfg.gatys || x->occ.size() != 1 || x->need_bott) return -1;
+    const Occ& o = x->occ[0];
+    if (o.ext == 31 || !x->tensor_in_style[o.tensor]) return -1;
+    if (o.off % 4 || o.ncol % 4 || x->ncc % 4) return -1;   // (float4 phi reads)
+    for (int u = 0; u < x->nu; ++u) if (x->uid[u] == o.tensor) return u;
+    return -1;
+}
+
 GramArgs gram_args(ast_ctx* x) {
     GramArgs g;
     memset(&g, 0, sizeof(g));
@@ -366,6 +381,7 @@ GramArgs gram_args(ast_ctx* x) {
     g.gpart = x->gpart; g.smat = x->smat; g.zero16 = x->zero;
     g.B = x->cfg.batch; g.T = x->cfg.T; g.nchunk = x->nchunk;
     g.top_u = -1; g.gmax_top = nullptr;
+    g.cont_u = -1;
     return g;
 }
 
@@ -531,8 +547,10 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     ALLOC(x->me, (size_t)x->nblk * c.batch * c.T * 16);
     ALLOC(x->chain[0], BTC * x->esz);
     ALLOC(x->chain[1], BTC * x->esz);
+    const int fuse_u = fused_content_occ(x);   // (the Gram backward adds that tap's gradient itself)
     for (int t = 0; t <= NBLK_MAX; ++t)
-        if (x->tensor_has_direct_content[t] || (t == 30 && x->need_bott)) ALLOC(x->cg_buf[t], BTC * x->esz);
+        if ((x->tensor_has_direct_content[t] && !(fuse_u >= 0 && x->uid[fuse_u] == t)) || (t == 30 && x->need_bott))
+            ALLOC(x->cg_buf[t], BTC * x->esz);
     if (x->need_bott) {
         ALLOC(x->bott, (size_t)c.batch * c.T * 16 * 4);
         ALLOC(x->gbott, (size_t)c.batch * c.T * 16 * 4);
@@ -803,7 +821,11 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     bool first_cg[NBLK_MAX + 1];
     for (int t = 0; t <= NBLK_MAX; ++t) first_cg[t] = true;
     bool first_bott = true;
+    const int fuse_u = fused_content_occ(x);
+    if (fuse_u >= 0)   // the Gram backward writes 64 of the occurrence's partial slots per clip
+        HIPCHK(hipMemsetAsync(x->cpart, 0, (size_t)c.batch * x->ncpart * 4, s));
     for (size_t i = 0; i < x->occ.size(); ++i) {
+        if (fuse_u >= 0) break;
         const Occ& o = x->occ[i];
         ContentArgs a;
         memset(&a, 0, sizeof(a));
@@ -852,6 +874,14 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
             g.gmax_top = x->gmax_g + (size_t)x->nblk * c.batch;
             HIPCHK(hipMemsetAsync(x->gmax_g, 0, (size_t)(NBLK_MAX + 1) * c.batch * 4, s));
             top_max_done = g.top_u >= 0;
+        }
+        if (fuse_u >= 0) {
+            const Occ& o = x->occ[0];
+            g.cg[fuse_u] = nullptr;
+            g.cont_u = fuse_u;
+            g.cont_phi = x->phi_c; g.cont_phi_bstride = x->phi_c_shared ? 0 : (size_t)c.T * x->ncc;
+            g.cont_ncc = x->ncc; g.cont_off = o.off; g.cont_ncol = o.ncol; g.cont_coef = ccoef;
+            g.cont_part = x->cpart; g.cont_pstride = (size_t)x->ncpart;
         }
         launch_gram_bwd_any(x, g, s);
     }

@@ -225,6 +225,15 @@ struct GramArgs {
     int B, T, nchunk;
     int top_u;                              // split bwd: unique tensor whose per-clip max |D| ...
     unsigned* gmax_top;                     // ... goes to gmax_top[b] (atomic max of float bits), or -1
+    // split bwd, fused content tap (methods.py:116-117): for unique tensor cont_u (or -1) D +=
+    // coef (E - phi[..., off + c]) on channels c < ncol, in place of k_content's cg buffer round
+    // trip; the workgroup's sum of squared errors goes to cont_part[b * cont_pstride + chunk *
+    // (C / 32) + channel group]
+    int cont_u;
+    const float* cont_phi; size_t cont_phi_bstride;
+    int cont_ncc, cont_off, cont_ncol;
+    float cont_coef;
+    float* cont_part; size_t cont_pstride;
 };
 
 struct StyleArgs {

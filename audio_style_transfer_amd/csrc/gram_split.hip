@@ -83,6 +83,19 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
     for (int cc = 0; cc < 4; ++cc)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[cc][i] = 0.f;
+    // fused content tap: the 128 threads whose output pieces are tensor cont_u's (iteration
+    // it = (cont_u % 16) / 4 of half cont_u / 16) load its E and phi one stage ahead
+    float4 ce = make_float4(0.f, 0.f, 0.f, 0.f), cp = ce;
+    const bool cthr = a.cont_u >= 0 && (((a.cont_u & 15) * 128) >> 9) * GWT + tid >= (a.cont_u & 15) * 128 &&
+                      (((a.cont_u & 15) * 128) >> 9) * GWT + tid < (a.cont_u & 15) * 128 + 128;
+    auto cload = [&](int t0) {
+        const int p = (((a.cont_u & 15) * 128) >> 9) * GWT + tid;
+        const int tt = (p >> 3) & 15, q = p & 7;
+        const size_t row = (size_t)b * a.T + t0 + tt;
+        ce = *reinterpret_cast<const float4*>((const float*)a.act + (size_t)a.uid[a.cont_u] * a.tstride + row * C + c0 + 4 * q);
+        cp = *reinterpret_cast<const float4*>(a.cont_phi + (size_t)b * a.cont_phi_bstride + (size_t)(t0 + tt) * a.cont_ncc + a.cont_off + c0 + 4 * q);
+    };
+    if (cthr) cload(tbeg);
     // two stages of loads in flight (v0 / v1 alternate; tlen is a multiple of 2 GSS)
     float4 v0[8], v1[8];
     auto load = [&](float4 (&v)[8], int t0) {
@@ -141,6 +154,7 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     float omax = 0.f;   // max |D| of tensor top_u (the backward chain's first input: no k_absmax pass)
+    float csd = 0.f;    // squared content error of tensor cont_u
     const int i16 = lane & 15, kq = lane >> 4;
     // A fragments (16x16x32): S~_c[u = 16 m + i16][u' = 8 kq .. + 8] as bf16 hi / lo; wave w
     // owns channels 4 w .. 4 w + 3
@@ -171,6 +185,19 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
         ld[k] = u < a.nu ? (const float*)a.act + (size_t)a.uid[u] * a.tstride + rowoff : (const float*)a.zero16;
         lrs[k] = u < a.nu ? C : 0;
     }
+    // fused content tap: the 128 threads whose output pieces are tensor cont_u's (iteration
+    // it = (cont_u % 16) / 4 of half cont_u / 16) load its E and phi one stage ahead
+    float4 ce = make_float4(0.f, 0.f, 0.f, 0.f), cp = ce;
+    const bool cthr = a.cont_u >= 0 && (((a.cont_u & 15) * 128) >> 9) * GWT + tid >= (a.cont_u & 15) * 128 &&
+                      (((a.cont_u & 15) * 128) >> 9) * GWT + tid < (a.cont_u & 15) * 128 + 128;
+    auto cload = [&](int t0) {
+        const int p = (((a.cont_u & 15) * 128) >> 9) * GWT + tid;
+        const int tt = (p >> 3) & 15, q = p & 7;
+        const size_t row = (size_t)b * a.T + t0 + tt;
+        ce = *reinterpret_cast<const float4*>((const float*)a.act + (size_t)a.uid[a.cont_u] * a.tstride + row * C + c0 + 4 * q);
+        cp = *reinterpret_cast<const float4*>(a.cont_phi + (size_t)b * a.cont_phi_bstride + (size_t)(t0 + tt) * a.cont_ncc + a.cont_off + c0 + 4 * q);
+    };
+    if (cthr) cload(tbeg);
     // two stages of loads in flight (v0 / v1 alternate; tlen is a multiple of 2 GSS)
     float4 v0[8], v1[8];
     auto load = [&](float4 (&v)[8], int t0) {
@@ -233,6 +260,17 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
                         const float4 g = *reinterpret_cast<const float4*>(cg + ((size_t)b * a.T + t0 + tt) * C + c0 + 4 * q);
                         o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
                     }
+                    if (u == a.cont_u) {   // the content tap, from E / phi loaded a stage ahead
+                        const int cc = c0 + 4 * q;
+                        const float ev[4] = {ce.x, ce.y, ce.z, ce.w}, pv[4] = {cp.x, cp.y, cp.z, cp.w};
+                        float d[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if (cc + i < a.cont_ncol) { d[i] = ev[i] - pv[i]; csd = fmaf(d[i], d[i], csd); }
+                        o.x += a.cont_coef * d[0]; o.y += a.cont_coef * d[1];
+                        o.z += a.cont_coef * d[2]; o.w += a.cont_coef * d[3];
+                        if (t0 + GSS < tend) cload(t0 + GSS);
+                    }
                     *reinterpret_cast<float4*>((float*)a.actw + off) = o;
                     if (u == a.top_u)
                         omax = fmaxf(omax, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
@@ -257,6 +295,19 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
 #pragma unroll
             for (int k = 1; k < GWT / 64; ++k) m = fmaxf(m, wm[k]);
             atomicMax(a.gmax_top + b, __float_as_uint(m));
+        }
+    }
+    if (a.cont_u >= 0) {  // the workgroup's content partial (a plain store: one slot per workgroup)
+        __shared__ float ws[GWT / 64];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) csd += __shfl_xor(csd, off);
+        if (lane == 0) ws[w] = csd;
+        __syncthreads();
+        if (tid == 0) {
+            float v = 0.f;
+#pragma unroll
+            for (int k = 0; k < GWT / 64; ++k) v += ws[k];
+            a.cont_part[(size_t)b * a.cont_pstride + ch * (C / GCS) + c0 / GCS] = v;
         }
     }
 }

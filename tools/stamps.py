@@ -33,7 +33,7 @@ if prec == 'bf16':
              'bwd: step 3 (mask, +tot, +D, stores)', '-', '-', '-', '-']
     tiles = B * T // 128 * 30 / 256   # tiles per CU over the 30 block launches
     groups = ((0, 4), (4, 8))
-elif os.environ.get('ASTYLE_FWD_ROLES', '1') != '0' and mode == 'fwd':
+elif os.environ.get('ASTYLE_FWD_ROLES', '0') != '0' and mode == 'fwd':
     # role-split forward (block_fwd_roles.hip): 4 dconv + 4 residual waves per CU
     names = {14: 'dconv: prologue + S_0', 6: 'dconv: GEMM1 half 0', 7: 'dconv: epi1 half 0', 8: 'dconv: GEMM1 half 1',
              9: 'dconv: epi1 half 1', 10: 'dconv: S wait', 13: 'resid: prologue + S_0', 12: 'resid: convert (period 0)',
