@@ -102,9 +102,22 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     RowUnits<MASKED, ONESEG> ru;
     ru.init(w, lane, ly, a.d);
     float4 lt[NU], lg[NU];
+    // unmasked layouts load through buffer resources of the tile (rs_t / rs_d, set with the tile)
+    rsrc_t rs_t, rs_d;
+    auto set_rs = [&](const Tile& t) {
+        if (!MASKED) {
+            rs_t = ru.rsrc_of(a.tin, t, a.T, a.d);
+            if (HAS_D) rs_d = ru.rsrc_of(a.dadd, t, a.T, a.d);
+        }
+    };
     auto load_unit = [&](const Tile& t, int k) {
-        lt[k] = ru.load(a.tin, t, k, a.T, a.fn, a.d);
-        if (HAS_D) lg[k] = ru.load(a.dadd, t, k, a.T, a.fn, a.d);
+        if (MASKED) {
+            lt[k] = ru.load(a.tin, t, k, a.T, a.fn, a.d);
+            if (HAS_D) lg[k] = ru.load(a.dadd, t, k, a.T, a.fn, a.d);
+        } else {
+            lt[k] = ru.loadb(rs_t, t, k, a.fn);
+            if (HAS_D) lg[k] = ru.loadb(rs_d, t, k, a.fn);
+        }
     };
     auto conv_unit = [&](int k, uint8_t* er, float s, uint32_t zb) {
         const float4 v = lt[k];
@@ -227,9 +240,13 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     // ---- epilogue unit (J, g) of tile et in three parts: residual read; out -> HBM; max ----
     float omax = 0.f, inv2p = 0.f;
     float* dst = nullptr;
+    rsrc_t rs_o;            // unmasked layouts: the stores through a resource at the tile's base time
+    const uint32_t colo[2] = {(uint32_t)((toff[0] * C + chb) * 4), (uint32_t)((toff[1] * C + chb) * 4)};
+    uint32_t ocol = 0;
     float4 oe, oo;
     auto epi_begin = [&](const Tile& et, int J) {
-        dst = a.gout + ((size_t)et.b * a.T + ctime(et, 32 * J + r, toff[J])) * C + chb;
+        if (MASKED) dst = a.gout + ((size_t)et.b * a.T + ctime(et, 32 * J + r, toff[J])) * C + chb;
+        else { rs_o = mk_rsrc(a.gout + ((size_t)et.b * a.T + et.tb) * C); ocol = colo[J]; }
     };
     auto epi_part = [&](int J, int g, int part, const uint8_t* er, uint32_t mw, float inv2) {
         if (part == 0) {
@@ -240,7 +257,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             oo.z = fmaf(keep_if(acc2[J][4 * g + 2], mw, 8 + g), inv2, oe.z);
             oo.w = fmaf(keep_if(acc2[J][4 * g + 3], mw, 12 + g), inv2, oe.w);
 #if !(defined(SW_EXP) && SW_EXP == 8)
-            *reinterpret_cast<float4*>(dst + 8 * g) = oo;
+            if (MASKED) *reinterpret_cast<float4*>(dst + 8 * g) = oo;
+            else bst4(rs_o, ocol + 32 * g, 0u, oo);
 #endif
         } else {
             omax = fmaxf(omax, fmaxf(fmaxf(fabsf(oo.x), fabsf(oo.y)), fmaxf(fabsf(oo.z), fabsf(oo.w))));
@@ -261,6 +279,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     float gm_c;     // max |tot| of the current tile's clip (one scalar load per tile: the next one's)
     {
         const Tile t0 = tile_of(blockIdx.x);
+        set_rs(t0);
 #pragma unroll
         for (int k = 0; k < NU; ++k) load_unit(t0, k);
         load_masks(t0, mu_c, muh_c, me_c);
@@ -270,6 +289,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
 #pragma unroll
         for (int k = 0; k < NU; ++k) conv_unit(k, &ER[0][0], s0, z0);
         const Tile t1 = tile_of(clampt(blockIdx.x + G));
+        set_rs(t1);
 #pragma unroll
         for (int k = 0; k < NU; ++k) load_unit(t1, k);
     }
@@ -281,6 +301,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         const Tile cu = tile_of(tile);
         const Tile nt = tile_of(clampt(tile + G));
         const Tile n2 = tile_of(clampt(tile + 2 * G));
+        set_rs(n2);   // (the previous ones' loads are all issued: units reload right after conversion)
         // T: this tile's tot image complete (converted during the previous phase C)
         lds_barrier();
         STAMP(6)

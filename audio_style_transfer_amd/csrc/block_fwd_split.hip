@@ -119,11 +119,13 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             ld[k] = *reinterpret_cast<const float4*>(src);
             return;
         }
-        const char* base = reinterpret_cast<const char*>(a.ein + ((ptrdiff_t)t.b * a.T + t.tb - a.d) * C);
+        // through a buffer resource at the tile's row-0 source: 32-bit lane offsets, no 64-bit
+        // address arithmetic per unit
+        const rsrc_t rs = mk_rsrc(a.ein + ((ptrdiff_t)t.b * a.T + t.tb - a.d) * C);
         uint32_t o = soff[k];
         if (ONESEG && k == 0 && lr == 0 && t.m0 == 0) o = row1;
         if (ONESEG && k == NU - 1 && lr == 1 && t.m0 + TMS >= a.n) o = row64;
-        ld[k] = *reinterpret_cast<const float4*>(base + o);
+        ld[k] = bld4(rs, o, 0u);
     };
     auto zero_bits_of = [&](const Tile& t) {
         uint32_t z = padz;
@@ -193,15 +195,18 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     // flush piece (j, q): columns 32 j + 8 q + lr (lr = lane >> 3), channels cq .. cq + 3; part 0
     // reads the row back, part 1 stores it
     float4 fl4;
+    const uint32_t fl_lane = (uint32_t)((lr * a.d * C + cq) * 4);
     auto flush_part = [&](int j, int q, int part, const uint8_t* erp) {
         const int c = 32 * j + 8 * q + lr;
         if (part == 0) {
             const int row = (MASKED || ONESEG) ? c + 1 : 34 * j + 1 + 8 * q + lr;   // frow(c)
             fl4 = *reinterpret_cast<const float4*>(erp + row * RS + 4 * cq);
-        } else {
-            const int t = MASKED ? pos_time(prv.p0 + c, a.fn, a.d)
-                                 : ONESEG ? prv.tb + c * a.d : prv.tb + j + (8 * q + lr) * a.d;
+        } else if (MASKED) {
+            const int t = pos_time(prv.p0 + c, a.fn, a.d);
             *reinterpret_cast<float4*>(a.eout + ((size_t)prv.b * a.T + t) * C + cq) = fl4;
+        } else {   // time tb + (uniform part) + lr d: the lane offset is fixed, the rest scalar
+            const int tu = ONESEG ? (32 * j + 8 * q) * a.d : j + 8 * q * a.d;
+            bst4(mk_rsrc(a.eout + ((size_t)prv.b * a.T + prv.tb) * C), fl_lane, (uint32_t)(tu * C * 4), fl4);
         }
     };
     // words and column times to LDS (all lanes write: identical values per column)

@@ -15,8 +15,8 @@
 //   bwd  D_c = S~_c E_c       v_mfma_f32_16x16x32_bf16 (A = S~_c halves in registers, B: lane
 //                             (t, kq): E_{8 kq .. + 8}[t][c]) from LDS images [c][t][u] (hi, lo);
 //                             D goes back through an fp32 image [u][t][c] in two halves of 16
-//                             tensors and leaves as whole 128-B lines, in place over E (+ the
-//                             content grad)
+//                             tensors and leaves as whole 128-B lines (+ the content grad: a
+//                             cg buffer, or the fused content tap computed here)
 // Loads and stores move whole 128-B lines (8 lanes x 16 B per row).
 #include "common.h"
 
@@ -83,19 +83,6 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
     for (int cc = 0; cc < 4; ++cc)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[cc][i] = 0.f;
-    // fused content tap: the 128 threads whose output pieces are tensor cont_u's (iteration
-    // it = (cont_u % 16) / 4 of half cont_u / 16) load its E and phi one stage ahead
-    float4 ce = make_float4(0.f, 0.f, 0.f, 0.f), cp = ce;
-    const bool cthr = a.cont_u >= 0 && (((a.cont_u & 15) * 128) >> 9) * GWT + tid >= (a.cont_u & 15) * 128 &&
-                      (((a.cont_u & 15) * 128) >> 9) * GWT + tid < (a.cont_u & 15) * 128 + 128;
-    auto cload = [&](int t0) {
-        const int p = (((a.cont_u & 15) * 128) >> 9) * GWT + tid;
-        const int tt = (p >> 3) & 15, q = p & 7;
-        const size_t row = (size_t)b * a.T + t0 + tt;
-        ce = *reinterpret_cast<const float4*>((const float*)a.act + (size_t)a.uid[a.cont_u] * a.tstride + row * C + c0 + 4 * q);
-        cp = *reinterpret_cast<const float4*>(a.cont_phi + (size_t)b * a.cont_phi_bstride + (size_t)(t0 + tt) * a.cont_ncc + a.cont_off + c0 + 4 * q);
-    };
-    if (cthr) cload(tbeg);
     // two stages of loads in flight (v0 / v1 alternate; tlen is a multiple of 2 GSS)
     float4 v0[8], v1[8];
     auto load = [&](float4 (&v)[8], int t0) {

@@ -180,6 +180,17 @@ struct RowUnits {
         if (ONESEG && k == NU - 1 && lr == 1 && t.m0 + TMS >= (int)fn.n) o = row64;
         return *reinterpret_cast<const float4*>(base + o);
     }
+    // unmasked layouts: the same rows through a buffer resource whose base is the tile's row-0
+    // source (rsrc_of): one 32-bit lane offset per unit instead of a 64-bit address
+    __device__ __forceinline__ rsrc_t rsrc_of(const float* src, const Tile& t, int T, int d) const {
+        return mk_rsrc(src + ((ptrdiff_t)t.b * T + t.tb - d) * C);
+    }
+    __device__ __forceinline__ float4 loadb(rsrc_t rs, const Tile& t, int k, const FDiv& fn) const {
+        uint32_t o = soff[k];
+        if (ONESEG && k == 0 && lr == 0 && t.m0 == 0) o = row1;
+        if (ONESEG && k == NU - 1 && lr == 1 && t.m0 + TMS >= (int)fn.n) o = row64;
+        return bld4(rs, o, 0u);
+    }
     __device__ __forceinline__ uint32_t zero_bits(const Tile& t, const FDiv& fn) const {
         uint32_t z = padz;
         if (ONESEG) {
