@@ -131,6 +131,7 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
 // backward.  Staging: thread (w, l) loads tensors 8 (w & 3) + k (k = 0..7), channel quad
 // l >> 3, row t0 + 8 (w >> 2) + (l & 7).  Output: 16 tensors at a time through O; padding
 // tensors (u >= nu) are neither read nor written.
+template <bool CONT>   // CONT: the fused content tap (a.cont_u >= 0); false: the round-2 kernel
 __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     __shared__ __attribute__((aligned(16))) u16 IH[GCS * GSS * BRS];       // [c][t][u] hi
     __shared__ __attribute__((aligned(16))) u16 IL[GCS * GSS * BRS];       // [c][t][u] lo
@@ -163,35 +164,37 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
         }
     // staging loads: tensors 8 uo + k, quad sq, row st of the stage
     const int uo = w & 3, sq = lane >> 3, st = 8 * (w >> 2) + (lane & 7);
-    const size_t rowoff = (size_t)b * a.T * C + c0 + 4 * sq;
+    // per tensor a wave-uniform base (the clip's first row; scalar registers) and one 32-bit lane
+    // offset for all eight (the tensors of a wave are uniform: uo = w & 3)
     const float* ld[8];
-    size_t lrs[8];
+    uint32_t lrs[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int u = 8 * uo + k;
-        ld[k] = u < a.nu ? (const float*)a.act + (size_t)a.uid[u] * a.tstride + rowoff : (const float*)a.zero16;
+        ld[k] = u < a.nu ? (const float*)a.act + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C : (const float*)a.zero16;
         lrs[k] = u < a.nu ? C : 0;
     }
+    const uint32_t lofs = (uint32_t)(c0 + 4 * sq);
     // fused content tap: the 128 threads whose output pieces are tensor cont_u's (iteration
-    // it = (cont_u % 16) / 4 of half cont_u / 16) load its E and phi one stage ahead
-    float4 ce = make_float4(0.f, 0.f, 0.f, 0.f), cp = ce;
-    const bool cthr = a.cont_u >= 0 && (((a.cont_u & 15) * 128) >> 9) * GWT + tid >= (a.cont_u & 15) * 128 &&
-                      (((a.cont_u & 15) * 128) >> 9) * GWT + tid < (a.cont_u & 15) * 128 + 128;
-    auto cload = [&](int t0) {
-        const int p = (((a.cont_u & 15) * 128) >> 9) * GWT + tid;
-        const int tt = (p >> 3) & 15, q = p & 7;
-        const size_t row = (size_t)b * a.T + t0 + tt;
-        ce = *reinterpret_cast<const float4*>((const float*)a.act + (size_t)a.uid[a.cont_u] * a.tstride + row * C + c0 + 4 * q);
-        cp = *reinterpret_cast<const float4*>(a.cont_phi + (size_t)b * a.cont_phi_bstride + (size_t)(t0 + tt) * a.cont_ncc + a.cont_off + c0 + 4 * q);
-    };
-    if (cthr) cload(tbeg);
+    // it = (cont_u % 16) / 4 of half cont_u / 16) load its E and phi rows at the start of each
+    // stage and add coef (E - phi) to those pieces (one copy of the code, not one per piece)
+    const int cit = ((a.cont_u & 15) * 128) >> 9;   // (wave-uniform test below)
+    const bool cthr = CONT && cit * GWT + tid >= (a.cont_u & 15) * 128 && cit * GWT + tid < (a.cont_u & 15) * 128 + 128;
+    const int cp_ = cit * GWT + tid, ctt = (cp_ >> 3) & 15, cq = cp_ & 7;
+    const float* ce_src = CONT ? (const float*)a.act + (size_t)a.uid[a.cont_u & 31] * a.tstride + (size_t)b * a.T * C + c0 + 4 * cq : nullptr;
+    const float* cp_src = CONT ? a.cont_phi + (size_t)b * a.cont_phi_bstride + a.cont_off + c0 + 4 * cq : nullptr;
     // two stages of loads in flight (v0 / v1 alternate; tlen is a multiple of 2 GSS)
     float4 v0[8], v1[8];
     auto load = [&](float4 (&v)[8], int t0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (size_t)(t0 + st) * lrs[k]);
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (lrs[k] ? lofs + (uint32_t)(t0 + st) * C : 0u));
     };
     auto stage = [&](float4 (&v)[8], int t0) {
+        float4 ce, cph;
+        if (CONT && cthr) {
+            ce = *reinterpret_cast<const float4*>(ce_src + (size_t)(t0 + ctt) * C);
+            cph = *reinterpret_cast<const float4*>(cp_src + (size_t)(t0 + ctt) * a.cont_ncc);
+        }
         uint4 fh[4], fl[4];   // channel 4 sq + j: tensors 8 uo .. + 8 at row st, hi / lo
         split8<0>(v, fh[0], fl[0]);
         split8<1>(v, fh[1], fl[1]);
@@ -223,6 +226,18 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
                                                                     __builtin_bit_cast(bf16x8, bl), c, 0, 0, 0);
             }
         }
+        float4 cadd = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (CONT && cthr) {
+            const int cc = c0 + 4 * cq;
+            const float ev[4] = {ce.x, ce.y, ce.z, ce.w}, pv[4] = {cph.x, cph.y, cph.z, cph.w};
+            float d[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                d[i] = cc + i < a.cont_ncol ? ev[i] - pv[i] : 0.f;
+                csd = fmaf(d[i], d[i], csd);
+            }
+            cadd = make_float4(a.cont_coef * d[0], a.cont_coef * d[1], a.cont_coef * d[2], a.cont_coef * d[3]);
+        }
         // lane holds D_c[u = 16 m + 4 kq + i][t = i16] for the wave's 4 channels
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
@@ -247,17 +262,7 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
                         const float4 g = *reinterpret_cast<const float4*>(cg + ((size_t)b * a.T + t0 + tt) * C + c0 + 4 * q);
                         o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
                     }
-                    if (u == a.cont_u) {   // the content tap, from E / phi loaded a stage ahead
-                        const int cc = c0 + 4 * q;
-                        const float ev[4] = {ce.x, ce.y, ce.z, ce.w}, pv[4] = {cp.x, cp.y, cp.z, cp.w};
-                        float d[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            if (cc + i < a.cont_ncol) { d[i] = ev[i] - pv[i]; csd = fmaf(d[i], d[i], csd); }
-                        o.x += a.cont_coef * d[0]; o.y += a.cont_coef * d[1];
-                        o.z += a.cont_coef * d[2]; o.w += a.cont_coef * d[3];
-                        if (t0 + GSS < tend) cload(t0 + GSS);
-                    }
+                    if (CONT && u == a.cont_u) { o.x += cadd.x; o.y += cadd.y; o.z += cadd.z; o.w += cadd.w; }
                     *reinterpret_cast<float4*>((float*)a.actw + off) = o;
                     if (u == a.top_u)
                         omax = fmaxf(omax, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
@@ -284,7 +289,7 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
             atomicMax(a.gmax_top + b, __float_as_uint(m));
         }
     }
-    if (a.cont_u >= 0) {  // the workgroup's content partial (a plain store: one slot per workgroup)
+    if (CONT) {           // the workgroup's content partial (a plain store: one slot per workgroup)
         __shared__ float ws[GWT / 64];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) csd += __shfl_xor(csd, off);
@@ -504,7 +509,8 @@ void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gram_bwd_f, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
 void launch_gram_bwd_s(const GramArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_gram_bwd_s, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+    if (a.cont_u >= 0) hipLaunchKernelGGL(k_gram_bwd_s<true>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+    else hipLaunchKernelGGL(k_gram_bwd_s<false>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
 
 }  // namespace ast
