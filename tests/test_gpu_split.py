@@ -319,3 +319,29 @@ def test_range_flags(weights, dev):
     eng.loss_grad(torch.tensor(x, dtype=torch.float32, device=dev))
     f = eng.range_flags().cpu().tolist()
     assert f[0] == 0 and f[1] & 2, f
+
+
+@pytest.mark.parametrize('cnt', [16, 10, 128])
+def test_fused_content_tap_channels(cnt, weights, dev):
+    """One content tap on a style-tapped tensor: the split Gram backward adds its gradient and
+    squared error itself (ASTYLE_FUSE_CONTENT, api.hip fused_content_occ) when cnt_channels is
+    a multiple of 4 (16, 128), else k_content's buffer path runs (10); both against the fp64
+    oracle at the fp32 bars, several clips with their own targets."""
+    T, B = 1024, 2
+    kw = dict(cont_ids=[29], style_ids=list(range(30)), gatys=False, nb_channels=128, cnt_channels=cnt)
+    rng = np.random.default_rng(11)
+    xs = [O.mu_law_numpy(synthetic_clips(1, T, 300 + b)[0]) for b in range(B)]
+    tg = [O.targets_from_audio(weights, xs[b], [O.mu_law_numpy(synthetic_clips(1, T, 900 + b)[0])], [xs[b]], **kw)
+          for b in range(B)]
+    x = np.stack([xs[b] + rng.normal(0, 6, T) for b in range(B)])
+    eng = _engine(B, T, kw, weights)
+    eng.set_targets(torch.tensor(np.stack([t[0] for t in tg]), dtype=torch.float32),
+                    torch.tensor(np.stack([t[1] for t in tg]), dtype=torch.float32))
+    parts, grad = eng.loss_grad(torch.tensor(x, dtype=torch.float32, device=dev))
+    parts, grad = parts.cpu().numpy(), grad.cpu().numpy()
+    for b in range(B):
+        ref_parts, ref_g = O.loss_and_grad(x[b], weights, phi_c=tg[b][0], phi_s=tg[b][1], lambd=100.0, **kw)
+        for k in range(4):
+            assert abs(parts[b, k] - ref_parts[k]) <= 1e-4 * abs(ref_parts[k]) + 1e-7, (cnt, b, k, parts[b], ref_parts)
+        e = rel(grad[b], ref_g)
+        assert e <= 2e-3, (cnt, b, e)
