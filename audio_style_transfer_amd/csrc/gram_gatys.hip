@@ -305,6 +305,24 @@ __device__ __forceinline__ void split2g(float x0, float x1, uint32_t& hi, uint32
     lo = pack2(x0 - bflo(hi), x1 - bfhi(hi));
 }
 
+// one 32x32 tile (I, J) of G (rows 32 I + (q & 3) + 8 (q >> 2) + 4 h, column 32 J + (lane & 31)),
+// and for an off-diagonal tile of the symmetric G its mirror (J, I): four 16-B stores per lane
+__device__ __forceinline__ void store_tile(float* G, int I, int J, const f32x16& acc, int lane) {
+    const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) G[(32 * I + (q & 3) + 8 * (q >> 2) + 4 * h) * C + 32 * J + col] = acc[q];
+    if (I != J) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(&G[(32 * J + col) * C + 32 * I + 8 * g + 4 * h]) =
+                make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+    }
+}
+
+// G = E^T E is symmetric: the 10 upper 32x32 tiles of the 4x4 grid are computed (waves 0 / 1:
+// the diagonal pairs {0, 1} / {2, 3} as (X0, X0), (X0, X1), (X1, X1); waves 2 / 3: block w - 2
+// against blocks 2 and 3) and the 6 off-diagonal ones are written twice: 30 instead of 48 MFMAs
+// per 16-row k-step and workgroup
 __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
     __shared__ __attribute__((aligned(1024))) u16 Lh[GYB * C];   // [t][c] bf16 hi, swizzled
     __shared__ __attribute__((aligned(1024))) u16 Ll[GYB * C];   // lo
@@ -314,7 +332,8 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
     const int nt = tlen / GYB;
     const float* E = (const float*)a.act + (size_t)a.uid[u] * a.tstride +
                      ((size_t)b * a.T + (size_t)ch * tlen) * C;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     // staging: float4 f = tid + 256 k: row (tid >> 5) + 8 k, channels 4 (tid & 31) .. + 3
     const int c4 = tid & 31, r0 = tid >> 5;
     float4 v[8];
@@ -327,23 +346,24 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
     // ((r & 3) << 2), half (c4 & 1)
     auto img = [&](int r) { return r * C + (((c4 >> 1) ^ ((r & 3) << 2)) * 8) + (c4 & 1) * 4; };
     const int kg = lane >> 5, g16 = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
-    int aoff[2], boff[2];
+    // fragment offset of channel block X (A and B fragments of G = E^T E coincide)
+    auto boff = [&](int X) { return (8 * kg + q) * C + (((4 * X + 2 * g16 + (p >> 1)) ^ (q << 2)) * 8) + (p & 1) * 4; };
+    const bool diag = w < 2;
+    const int X0 = diag ? 2 * w : w - 2;     // diagonal waves: blocks X0, X0 + 1; others: A = X0
+    const int o0 = boff(X0), o1 = boff(diag ? X0 + 1 : 2), o2 = boff(3);
+    f32x16 acc[3];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int I = 2 * (w >> 1) + t, J = 2 * (w & 1) + t;
-        aoff[t] = (8 * kg + q) * C + (((4 * I + 2 * g16 + (p >> 1)) ^ (q << 2)) * 8) + (p & 1) * 4;
-        boff[t] = (8 * kg + q) * C + (((4 * J + 2 * g16 + (p >> 1)) ^ (q << 2)) * 8) + (p & 1) * 4;
-    }
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-            for (int e = 0; e < 16; ++e) acc[ii][jj][e] = 0.f;
+    for (int i = 0; i < 3; ++i)
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
     auto frag = [&](const u16* L, int off, int s) {
         const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(L + off + (16 * s) * C));
         const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(L + off + (16 * s + 4) * C));
         return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    auto mm3 = [&](f32x16& c, const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl) {
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
     };
     load(0);
     for (int k = 0; k < nt; ++k) {
@@ -361,25 +381,28 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
         __syncthreads();
 #pragma unroll
         for (int s = 0; s < GYB / 16; ++s) {
-            bf16x8 fah[2], fal[2], fbh[2], fbl[2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                fah[t] = frag(Lh, aoff[t], s);
-                fal[t] = frag(Ll, aoff[t], s);
-                fbh[t] = frag(Lh, boff[t], s);
-                fbl[t] = frag(Ll, boff[t], s);
+            const bf16x8 h0 = frag(Lh, o0, s), l0 = frag(Ll, o0, s);
+            const bf16x8 h1 = frag(Lh, o1, s), l1 = frag(Ll, o1, s);
+            if (diag) {
+                mm3(acc[0], h0, l0, h0, l0);     // (X0, X0)
+                mm3(acc[1], h0, l0, h1, l1);     // (X0, X0 + 1)
+                mm3(acc[2], h1, l1, h1, l1);     // (X0 + 1, X0 + 1)
+            } else {
+                const bf16x8 h2 = frag(Lh, o2, s), l2 = frag(Ll, o2, s);
+                mm3(acc[0], h0, l0, h1, l1);     // (X0, 2)
+                mm3(acc[1], h0, l0, h2, l2);     // (X0, 3)
             }
-#pragma unroll
-            for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-                for (int jj = 0; jj < 2; ++jj) {
-                    acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fah[ii], fbh[jj], acc[ii][jj], 0, 0, 0);
-                    acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fah[ii], fbl[jj], acc[ii][jj], 0, 0, 0);
-                    acc[ii][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fal[ii], fbh[jj], acc[ii][jj], 0, 0, 0);
-                }
         }
     }
-    store_gpart(a, b, u, ch, acc, w, lane);
+    float* G = a.gpart + (((size_t)b * a.nchunk + ch) * a.nu + u) * (C * C);
+    if (diag) {
+        store_tile(G, X0, X0, acc[0], lane);
+        store_tile(G, X0, X0 + 1, acc[1], lane);
+        store_tile(G, X0 + 1, X0 + 1, acc[2], lane);
+    } else {
+        store_tile(G, X0, 2, acc[0], lane);
+        store_tile(G, X0, 3, acc[1], lane);
+    }
 }
 
 __global__ void __launch_bounds__(256) k_gatys_bwd_s(GatysArgs a) {
