@@ -299,7 +299,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             acc1[J] = mfma_f16(wd[tp][kb][0], xh, acc1[J]);
             if (st + LA < 24) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
             side(st);
+#if !(defined(SW_EXP) && SW_EXP == 20)   // (timing experiment: drop the w_lo products)
             acc1[J] = mfma_f16(wd[tp][kb][1], xh, acc1[J]);
+#endif
             acc1[J] = mfma_f16(wd[tp][kb][0], xl, acc1[J]);
             step3_schedule();
         }
@@ -323,7 +325,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             acc2[J] = mfma_f16(wr[kb][0], bh[cb], acc2[J]);
             if (kb + LA < 8) bload(kb + LA, bh[(kb + LA) % (LA + 1)], bl[(kb + LA) % (LA + 1)]);
             side(kb);
+#if !(defined(SW_EXP) && SW_EXP == 20)
             acc2[J] = mfma_f16(wr[kb][1], bh[cb], acc2[J]);
+#endif
             acc2[J] = mfma_f16(wr[kb][0], bl[cb], acc2[J]);
             step3_schedule();
         }
