@@ -247,6 +247,8 @@ static bool d_out_of_place() {
     return v != 0;
 }
 
+int fused_content_occ(const ast_ctx* x);
+
 size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     const size_t BTC = (size_t)c->batch * c->T * C;
     const size_t es = c->precision == 1 ? 2 : 4;
@@ -257,8 +259,9 @@ size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     n += 2 * (size_t)x->nblk * c->batch * c->T * 16;        // mu, me
     n += 2 * BTC * es;                                      // chain
     int ncg = 0;
+    const int fuse_u = fused_content_occ(x);   // (as ast_create: no content-gradient buffer for it)
     for (int t = 0; t <= NBLK_MAX; ++t)
-        if (x->tensor_has_direct_content[t] || (t == 30 && x->need_bott)) ++ncg;
+        if ((x->tensor_has_direct_content[t] && !(fuse_u >= 0 && x->uid[fuse_u] == t)) || (t == 30 && x->need_bott)) ++ncg;
     n += (size_t)ncg * BTC * es;
     if (x->need_bott) n += 2 * (size_t)c->batch * c->T * 16 * 4;
     n += x->gpart_elems * 4;                                // gpart
@@ -368,7 +371,7 @@ void launch_gram_bwd_any(ast_ctx* x, const GramArgs& g, hipStream_t s) {
 int fused_content_occ(const ast_ctx* x) {
     static int en = -1;
     if (en < 0) { const char* e = getenv("ASTYLE_FUSE_CONTENT"); en = e ? (atoi(e) != 0) : 1; }
-    if (!en || !x->split || x->cfg.gatys || x->occ.size() != 1 || x->need_bott) return -1;
+    if (!en || x->cfg.precision != 2 || x->cfg.gatys || x->occ.size() != 1 || x->need_bott) return -1;
     const Occ& o = x->occ[0];
     if (o.ext == 31 || !x->tensor_in_style[o.tensor]) return -1;
     if (o.off % 4 || o.ncol % 4 || x->ncc % 4) return -1;   // (float4 phi reads)
