@@ -75,8 +75,12 @@ def _ws(**kw):
 def test_workspace_scales_with_precision_and_blocks():
     rc32, n32, _ = _ws(precision=0)
     rc16, n16, _ = _ws(precision=1)
-    rcs, ns, _ = _ws(precision=2)
+    rcs, ns, _ = _ws(precision=2, cnt=10)   # 10 content channels: not the fused content tap
     assert rc32 == 0 and rc16 == 0 and rcs == 0 and n16 < n32 < ns   # split: + fp16 fragments
+    # split with one style-tapped content layer of 128 channels: the Gram backward adds the
+    # content gradient itself, so no B x T x 128 fp32 content-gradient buffer
+    rcf, nf, _ = _ws(precision=2)
+    assert rcf == 0 and nf == ns - 2 * 16384 * 128 * 4
     # stack 0 + content 25 runs 26 blocks (TF prunes the rest)
     rc, n26, _ = _ws(cont=[25], style=list(range(10)))
     assert rc == 0 and n26 < n32
