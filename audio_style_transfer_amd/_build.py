@@ -11,7 +11,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, 'csrc')
 LIB = os.path.join(PKG, 'libastyle.so')
 SOURCES = ['encoder.hip', 'block_fwd_bf16.hip', 'block_bwd_bf16.hip', 'block_fwd_split.hip',
-           'block_bwd_split.hip', 'block_fwd_roles.hip', 'gram.hip', 'gram_bf16.hip', 'gram_split.hip', 'gram_gatys.hip', 'stft_reg.hip',
+           'block_bwd_split.hip', 'block_fwd_roles.hip', 'block_fwd_db.hip', 'gram.hip', 'gram_bf16.hip', 'gram_split.hip', 'gram_gatys.hip', 'stft_reg.hip',
            'lbfgs.hip', 'ot_admm.hip', 'api.hip', 'ckpt.cpp']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 CXX = os.environ.get('CXX', 'g++')          # host-only sources (.cpp)
@@ -24,7 +24,7 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall',
 # index the register-resident weight arrays dynamically and demote them to scratch)
 _CW = ['-mllvm', '-amdgpu-mfma-vgpr-form=1', '-mllvm', '-amdgpu-atomic-optimizer-strategy=None', '-mllvm', '-pragma-unroll-threshold=1000000', '-fno-slp-vectorize']
 EXTRA = {'block_fwd_bf16.hip': _CW, 'block_bwd_bf16.hip': _CW, 'block_fwd_split.hip': _CW,
-         'block_bwd_split.hip': _CW, 'block_fwd_roles.hip': _CW}
+         'block_bwd_split.hip': _CW, 'block_fwd_roles.hip': _CW, 'block_fwd_db.hip': _CW}
 
 
 def _stale() -> bool:

@@ -1,47 +1,42 @@
-// Split-fp16 encoder block forward (precision 2): model.py:95-116 for one block,
-//   u = dconv_d(relu(e_l)) + b_d        (masked.py:110-160, K = 3, SAME zero padding)
-//   e_{l+1} = e_l + W_r^T relu(u) + b_r
-// fp32 storage, v_mfma_f32_32x32x16_f16 on split fp16 operands, fp32 accumulation and fp32
-// epilogues (splitwave.h).
-//
-// One workgroup per CU (wave w owns output channels 32 w .. 32 w + 31), persistent over tiles
-// of 64 positions, one wave per SIMD: every epilogue runs in the shadow of MFMAs.  The two
-// 32-column halves j of a tile are separate MFMA phases, so the epilogue of one half overlaps
-// the GEMM of the other.  A tile's e_l arrives in registers (rows: unit k = image rows 8 k ..
-// 8 k + 7 x wave w's 32 channels, 8 cache lines per wave instruction), loaded during phases A
-// and B of the previous tile, and is converted into the LDS image (split relu(e_l), scaled by
-// 2^m_e from the clip's max |e_l|) and into the wave's quarter of a residual buffer (fp32 e_l,
-// double-buffered, read back by the same wave only).  Per tile i:
+// Split-fp16 encoder block forward (precision 2), double-buffered image variant: the same
+// block as block_fwd_split.hip (model.py:95-116, masked.py:110-160) with the same arithmetic in
+// the same order (bit-identical results), scheduled differently.  block_fwd_split.hip keeps two
+// fp32 residual buffers (the conversion writes tile i+1's e_l rows while tile i's wait for
+// epilogue 2), so its single split image can only be refilled under GEMM 2's half 1 (24 MFMAs,
+// the conversion's VALU and LDS writes exposed).  Here ONE staging buffer OB takes a tile's
+// e_l again as whole lines from L2 / the Infinity Cache (its rows were loaded two tiles
+// earlier), so the 38 KB freed double-buffers the image and the conversion of tile i+1 runs
+// under tile i's GEMM-1 phases (144 MFMAs); the row loads move one tile further ahead.
+// Per tile i (image slot i & 1):
 //   T  barrier (image i complete)
-//   A  GEMM 1, column half 0 (3 taps x 8 k-blocks x 3 products); carries epilogue 2 of tile
-//      i-1 (8 units of 3 steps: e_i = e_{i-1} + y + b_r back into the residual rows, e > 0
-//      bits, max |e|), the flush of its half 0 (residual rows -> HBM as whole lines) and the
-//      row loads of tile i+1, units 0..4
-//   B  GEMM 1, column half 1; carries epilogue 1 of half 0 (u = acc 2^-(m_e+k_d) + b_d, u > 0
-//      bits, v = relu(u) 2^m_v -> split v image; m_v from the bound |u| <= wdn max|e_l| + bdm),
-//      the flush of epilogue 2's half 1 and the row loads of units 5..8; barrier
-//   C  GEMM 2 (8 k-blocks x 3 products), half 0; carries epilogue 1 of half 1; barrier
-//   D  GEMM 2, half 1; carries the conversion of tile i+1 (image + residual)
-// Round-2 measurements of this structure: ~13k cycles per tile against an MFMA
-// floor of 6.2k; moving the loads / conversions between phases does not change the tile time.
+//   A  GEMM 1 half 0 over image i; tile i's residual rows (8 whole-line loads); epilogue 2 of
+//      tile i-1 in OB (e_i = e_{i-1} + y + b_r in place) and the flush of its half 0 (whole
+//      lines -> HBM); conversion of tile i+1 units 0..4 into image i+1, row loads of tile i+2
+//   B  GEMM 1 half 1; epilogue 1 of half 0, the flush of half 1, conversion units 5..8 +
+//      loads; barrier
+//   C  GEMM 2 half 0; epilogue 1 of half 1; barrier
+//   D  GEMM 2 half 1; tile i's residual rows -> OB
+// Scattering e_l / e_{l+1} in the accumulator layout instead (32 lines per wave instruction)
+// made the launch 7-14 % slower than block_fwd_split.hip, and this form is 5 % slower
+// (the conversion costs as many cycles under GEMM 1 as under GEMM 2).
+// ASTYLE_FWD_DB selects it (block_fwd_split.hip's launcher).
 #include "splitwave.h"
 #include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 
 namespace ast {
 namespace {
 using namespace sw;
 
-constexpr int IROWS = 72;             // image / residual rows: 66 or 68 used, 9 units x 8 rows
-constexpr int ISLOT = IROWS * RS;     // bytes per image / residual buffer
+constexpr int IROWS = 72;             // image rows: 66 or 68 used, 9 units x 8 rows
+constexpr int ISLOT = IROWS * RS;     // bytes per image
 constexpr int LA = 2;                 // B-fragment lookahead (steps)
 
 template <bool MASKED, bool ONESEG>
-__global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
-    __shared__ __attribute__((aligned(16))) uint8_t IMG[ISLOT];     // split relu(e_l) image
-    __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];   // fp32 e_l (residual) rows
+__global__ void __launch_bounds__(FT, 1) k_block_fwd_db(FwdArgsS a, Layout ly) {
+    __shared__ __attribute__((aligned(16))) uint8_t IMG[2][ISLOT];  // split relu(e_l) images
     __shared__ __attribute__((aligned(16))) uint8_t XV[TMS * RS];   // split v image
+    __shared__ __attribute__((aligned(16))) uint8_t OB[ISLOT];      // residual -> e_{l+1} rows (staging)
     __shared__ __attribute__((aligned(16))) float BIAS[2 * C];      // b_d, b_r
     __shared__ __attribute__((aligned(16))) float BDS[C];           // b_d 2^m_v (the current clip's v scale)
     __shared__ __attribute__((aligned(16))) uint16_t MBU[TMS * 8];  // u > 0 words of the tile
@@ -57,11 +52,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     STAMP_DECL
 
     auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, a.ft, a.fn, a.d, ly); };
-    // tiles past the end repeat the last one (loaded and converted, never used)
     auto clampt = [&](int tl) { return tl < ntiles ? tl : ntiles - 1; };
 
-    // this wave's split weight halves, resident in AGPRs for the whole launch: every load is
-    // issued before the first pin (a pin right after its load would wait for it)
     uint4 wd[3][8][2], wr[8][2];
 #pragma unroll
     for (int tp = 0; tp < 3; ++tp)
@@ -87,15 +79,10 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     const int chb = 32 * w + 4 * h;   // first channel of this lane's accumulator group g = 0
     auto ctime = [&](const Tile& t, int cc, int to) { return col_time<MASKED>(t, cc, to, a.fn, a.d); };
 
-    // ---- row units: unit k, lane -> image row L = 8 k + lr, channels cq .. cq + 3 ----
+    // ---- row units (as block_fwd_split.hip): unit k, lane -> image row 8 k + lr ----
     const int lr = lane >> 3;
     const int cq = 32 * w + 4 * (lane & 7);
-    const uint32_t imgo = (uint32_t)(lr * RS + 2 * cq);   // + 8 k RS: split row bytes
-    const uint32_t ero = (uint32_t)(lr * RS + 4 * cq);    // + 8 k RS: fp32 row bytes
-    // unmasked layouts: byte offset of the unit's source row from the tile's row-0 source
-    // (time tb - d); rows without a source (pad rows, rows past the image) read row 1 and are
-    // zeroed (bit k of padz); one-segment halos (unit 0 row 0, unit 8 row 65) are decided per
-    // tile.  Masked layouts: only rows past 65 are unused
+    const uint32_t imgo = (uint32_t)(lr * RS + 2 * cq);
     uint32_t soff[NU];
     uint32_t padz = 0;
 #pragma unroll
@@ -105,27 +92,25 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         if (none) padz |= 1u << k;
         soff[k] = MASKED ? 0u : (uint32_t)(((none ? 0 : row_toff(L, ly, a.d)) + a.d) * C * 4 + 4 * cq);
     }
-    const uint32_t row1 = (uint32_t)(a.d * C * 4 + 4 * cq), row64 = (uint32_t)(TMS * a.d * C * 4 + 4 * cq);   // image row 64 (time tb + 63 d)
+    const uint32_t row1 = (uint32_t)(a.d * C * 4 + 4 * cq), row64 = (uint32_t)(TMS * a.d * C * 4 + 4 * cq);
 
     float4 ld[NU];          // rows of the next tile to convert
+    rsrc_t rs_l;            // unmasked: the loading tile's row-0 source (set with the tile)
+    auto set_load_tile = [&](const Tile& t) {
+        if (!MASKED) rs_l = mk_rsrc(a.ein + ((ptrdiff_t)t.b * a.T + t.tb - a.d) * C);
+    };
     auto load_unit = [&](const Tile& t, int k) {
         if (MASKED) {
             const int L = 8 * k + lr;
-            // row L = position p0 + L - 1, clamped into the clip (rows 0 / 65 are real
-            // neighbours when the tile starts / ends inside a sub-sequence; the tap masks of
-            // gemm1h drop the ones outside a column's sub-sequence)
             const int pp = (padz >> k) & 1u ? t.p0 : min(max(t.p0 + L - 1, 0), a.T - 1);
             const float* src = a.ein + ((size_t)t.b * a.T + pos_time(pp, a.fn, a.d)) * C + cq;
             ld[k] = *reinterpret_cast<const float4*>(src);
             return;
         }
-        // through a buffer resource at the tile's row-0 source: 32-bit lane offsets, no 64-bit
-        // address arithmetic per unit
-        const rsrc_t rs = mk_rsrc(a.ein + ((ptrdiff_t)t.b * a.T + t.tb - a.d) * C);
         uint32_t o = soff[k];
         if (ONESEG && k == 0 && lr == 0 && t.m0 == 0) o = row1;
         if (ONESEG && k == NU - 1 && lr == 1 && t.m0 + TMS >= a.n) o = row64;
-        ld[k] = bld4(rs, o, 0u);
+        ld[k] = bld4(rs_l, o, 0u);
     };
     auto zero_bits_of = [&](const Tile& t) {
         uint32_t z = padz;
@@ -135,22 +120,20 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         }
         return z;
     };
-    // conversion of unit k: raw fp32 -> residual buffer er; relu, scale, split -> image
-    auto conv_unit = [&](int k, uint8_t* er, float s, uint32_t zb) {
+    // conversion of unit k: relu, scale, split -> image img
+    auto conv_unit = [&](int k, uint8_t* img, float s, uint32_t zb) {
         float4 v = ld[k];
-        *reinterpret_cast<float4*>(er + ero + 8 * k * RS) = v;
         const float sk = (zb >> k) & 1u ? 0.f : s;
         v.x = __int_as_float(max(__float_as_int(v.x), 0)); v.y = __int_as_float(max(__float_as_int(v.y), 0));
         v.z = __int_as_float(max(__float_as_int(v.z), 0)); v.w = __int_as_float(max(__float_as_int(v.w), 0));
         uint32_t h01, l01, h23, l23;
         split2(v.x * sk, v.y * sk, h01, l01);
         split2(v.z * sk, v.w * sk, h23, l23);
-        uint8_t* p = IMG + imgo + 8 * k * RS;
+        uint8_t* p = img + imgo + 8 * k * RS;
         *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
         *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
     };
 
-    // e_{l+1} > 0 words of a finished tile -> next layer's positions (wave w: columns 16 w..)
     auto store_me = [&](int b) {
         if (a.me_next && lane < 16) {
             const int c = 16 * w + lane;
@@ -161,55 +144,64 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         }
     };
 
-    // ---- epilogue 2 of tile prv (residual rows erp), unit u = (j, g) in three parts.  e_{l+1}
-    //      goes back into the residual rows it was computed from (in place: only this wave reads
-    //      its quarter), and leaves for HBM from there as whole 128-B lines (flush: 8 columns x
-    //      the wave's 32 channels per store); stored straight from the accumulator layout, each
-    //      store would touch 32 lines 32 B at a time ----
-    f32x16 acc2[2];                    // y of the pending epilogue 2
+    // ---- the staging rows OB (this wave's quarter, private to it): piece (j, q) = columns
+    //      32 j + 8 q + lr, channels cq .. cq + 3, at image row frow(c); the tile's residual e_l
+    //      comes in as whole lines (loaded in its phase A, written in its phase D), epilogue 2
+    //      turns it into e_{l+1} in place, and the flush stores the rows as whole lines ----
+    const uint32_t fl_lane = (uint32_t)((lr * a.d * C + cq) * 4);
+    auto piece_row = [&](int j, int q) { return (MASKED || ONESEG) ? 32 * j + 8 * q + lr + 1 : 34 * j + 1 + 8 * q + lr; };
+    auto piece_tu = [&](int j, int q) { return ONESEG ? (32 * j + 8 * q) * a.d : j + 8 * q * a.d; };
+    float4 rrow[8];
+    auto rr_load = [&](const Tile& t, int p) {
+        const int j = p >> 2, q = p & 3;
+        if (MASKED) {
+            const int tm = pos_time(t.p0 + 32 * j + 8 * q + lr, a.fn, a.d);
+            rrow[p] = *reinterpret_cast<const float4*>(a.ein + ((size_t)t.b * a.T + tm) * C + cq);
+        } else {
+            rrow[p] = bld4(mk_rsrc(a.ein + ((ptrdiff_t)t.b * a.T + t.tb) * C), fl_lane, (uint32_t)(piece_tu(j, q) * C * 4));
+        }
+    };
+    auto rr_write = [&](int p) {
+        *reinterpret_cast<float4*>(OB + piece_row(p >> 2, p & 3) * RS + 4 * cq) = rrow[p];
+    };
+
+    // ---- epilogue 2 of tile prv, unit u = (j, g) in three parts: residual read; e_{l+1} back
+    //      into the staging rows; bits, max ----
+    f32x16 acc2[2];
     Tile prv = tile_of(blockIdx.x);
     float inv2p = 0.f;
     float emax = 0.f;
     uint32_t mb[2] = {0u, 0u};
     float4 e2e, e2b, e2o;
-    auto epi2_begin = [&]() {   // (emax runs on over the workgroup's consecutive tiles of one clip)
-        mb[0] = mb[1] = 0u;
-    };
-    auto epi2_part = [&](int u, int part, uint8_t* erp) {
+    auto epi2_begin = [&]() { mb[0] = mb[1] = 0u; };
+    auto epi2_part = [&](int u, int part) {
         const int j = u >> 2, g = u & 3;
         if (part == 0) {
-            e2e = *reinterpret_cast<const float4*>(erp + Lc[j] * RS + 4 * (chb + 8 * g));
+            e2e = *reinterpret_cast<const float4*>(OB + Lc[j] * RS + 4 * (chb + 8 * g));
             e2b = *reinterpret_cast<const float4*>(&BIAS[C + chb + 8 * g]);
         } else if (part == 1) {
             e2o.x = e2e.x + fmaf(acc2[j][4 * g + 0], inv2p, e2b.x);
             e2o.y = e2e.y + fmaf(acc2[j][4 * g + 1], inv2p, e2b.y);
             e2o.z = e2e.z + fmaf(acc2[j][4 * g + 2], inv2p, e2b.z);
             e2o.w = e2e.w + fmaf(acc2[j][4 * g + 3], inv2p, e2b.w);
-            *reinterpret_cast<float4*>(erp + Lc[j] * RS + 4 * (chb + 8 * g)) = e2o;
+            *reinterpret_cast<float4*>(OB + Lc[j] * RS + 4 * (chb + 8 * g)) = e2o;
         } else {
             emax = fmaxf(emax, fmaxf(fmaxf(fabsf(e2o.x), fabsf(e2o.y)), fmaxf(fabsf(e2o.z), fabsf(e2o.w))));
-            // bit mbit(4 g + q) = 4 q + g of the column's word (common.h)
             mb[j] = or_pos_bits4(mb[j], e2o.x, e2o.y, e2o.z, e2o.w, g);
         }
     };
-    // flush piece (j, q): columns 32 j + 8 q + lr (lr = lane >> 3), channels cq .. cq + 3; part 0
-    // reads the row back, part 1 stores it
+    // flush piece (j, q) of tile prv: part 0 reads the row back, part 1 stores it
     float4 fl4;
-    const uint32_t fl_lane = (uint32_t)((lr * a.d * C + cq) * 4);
-    auto flush_part = [&](int j, int q, int part, const uint8_t* erp) {
-        const int c = 32 * j + 8 * q + lr;
+    auto flush_part = [&](int j, int q, int part) {
         if (part == 0) {
-            const int row = (MASKED || ONESEG) ? c + 1 : 34 * j + 1 + 8 * q + lr;   // frow(c)
-            fl4 = *reinterpret_cast<const float4*>(erp + row * RS + 4 * cq);
+            fl4 = *reinterpret_cast<const float4*>(OB + piece_row(j, q) * RS + 4 * cq);
         } else if (MASKED) {
-            const int t = pos_time(prv.p0 + c, a.fn, a.d);
+            const int t = pos_time(prv.p0 + 32 * j + 8 * q + lr, a.fn, a.d);
             *reinterpret_cast<float4*>(a.eout + ((size_t)prv.b * a.T + t) * C + cq) = fl4;
-        } else {   // time tb + (uniform part) + lr d: the lane offset is fixed, the rest scalar
-            const int tu = ONESEG ? (32 * j + 8 * q) * a.d : j + 8 * q * a.d;
-            bst4(mk_rsrc(a.eout + ((size_t)prv.b * a.T + prv.tb) * C), fl_lane, (uint32_t)(tu * C * 4), fl4);
+        } else {
+            bst4(mk_rsrc(a.eout + ((size_t)prv.b * a.T + prv.tb) * C), fl_lane, (uint32_t)(piece_tu(j, q) * C * 4), fl4);
         }
     };
-    // words and column times to LDS (all lanes write: identical values per column)
     auto epi2_words = [&]() {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -218,21 +210,16 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             MBT[c] = ctime(prv, c, toff[j]);
         }
     };
-    // max |e_{l+1}| of clip prv.b -> gmax_out, once per run of tiles of one clip (with the
-    // clip-interleaved tile order a workgroup usually keeps its clip for the whole launch)
     auto epi2_max = [&]() {
         const uint32_t m = wave_max_bits(emax);
         if (lane == 0) atomicMax(a.gmax_out + prv.b, m);
         emax = 0.f;
     };
 
-    // ---- epilogue 1 of column half j, unit g in two parts: u, bits; v -> split v image ----
-    // v = relu(u) 2^m_v = relu(acc 2^(m_v - m_e - k_d) + b_d 2^m_v): the scale folded into the fma
-    // (powers of two: the same values); the u > 0 bits from the split's rtz hi halves (splitwave.h
-    // nz2; SW_UBITS_EXACT: from v itself)
+    // ---- epilogue 1 (as block_fwd_split.hip) ----
     f32x16 acc1[2];
     float a1 = 0.f;
-    float bs_sv = -1.f;   // the v scale BDS holds
+    float bs_sv = -1.f;
     uint32_t mu_w = 0;
     float4 e1v;
     auto epi1_part = [&](int j, int g, int part) {
@@ -265,8 +252,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         }
     };
 
-    // ---- GEMM 1 of column half J over the image; side work per step ----
-    auto gemm1h = [&](auto j_tag, auto side, const Tile& cu) {
+    // ---- GEMM 1 of column half J over image img ----
+    auto gemm1h = [&](auto j_tag, auto side, const Tile& cu, const uint8_t* img) {
         constexpr int J = decltype(j_tag)::value;
         bool ok0 = true, ok2 = true;
         if (MASKED) {
@@ -277,12 +264,10 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc1[J][i] = 0.f;
-        // B fragments are read LA steps ahead (a step is only 3 MFMAs: one step ahead leaves
-        // the LDS latency exposed)
         uint4 bh[LA + 1], bl[LA + 1];
         auto bread = [&](int st, uint4& xh, uint4& xl) {
             const int tp = st >> 3, kb = st & 7;
-            const uint8_t* p = IMG + (Lc[J] + tp - 1) * RS + kb * 32 + h * 16;
+            const uint8_t* p = img + (Lc[J] + tp - 1) * RS + kb * 32 + h * 16;
             xh = lds16(p);
             xl = lds16(p + 256);
         };
@@ -299,14 +284,11 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             acc1[J] = mfma_f16(wd[tp][kb][0], xh, acc1[J]);
             if (st + LA < 24) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
             side(st);
-#if !(defined(SW_EXP) && SW_EXP == 20)   // (timing experiment: drop the w_lo products)
             acc1[J] = mfma_f16(wd[tp][kb][1], xh, acc1[J]);
-#endif
             acc1[J] = mfma_f16(wd[tp][kb][0], xl, acc1[J]);
             step3_schedule();
         }
     };
-    // ---- GEMM 2 of column half J over the v image ----
     auto gemm2h = [&](auto j_tag, auto side) {
         constexpr int J = decltype(j_tag)::value;
 #pragma unroll
@@ -325,9 +307,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             acc2[J] = mfma_f16(wr[kb][0], bh[cb], acc2[J]);
             if (kb + LA < 8) bload(kb + LA, bh[(kb + LA) % (LA + 1)], bl[(kb + LA) % (LA + 1)]);
             side(kb);
-#if !(defined(SW_EXP) && SW_EXP == 20)
             acc2[J] = mfma_f16(wr[kb][1], bh[cb], acc2[J]);
-#endif
             acc2[J] = mfma_f16(wr[kb][0], bl[cb], acc2[J]);
             step3_schedule();
         }
@@ -337,29 +317,32 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
 
     if (blockIdx.x >= ntiles) return;   // (grid = min(tiles, CUs): not taken)
 
-    // prologue: the first tile's image and residual rows; the second tile's rows in flight
-    float gm_c;     // max |e_l| of the current tile's clip (one scalar load per tile: the next one's)
+    // prologue: the first tile's image; the second tile's rows in flight
+    float gm_c;     // max |e_l| of the current tile's clip (at the top: the next one's)
     {
         const Tile t0 = tile_of(blockIdx.x);
+        set_load_tile(t0);
 #pragma unroll
         for (int k = 0; k < NU; ++k) load_unit(t0, k);
         const uint32_t z0 = zero_bits_of(t0);
         gm_c = sload(a.gmax_in + t0.b);
         const float s0 = exp2i(scale_exp(gm_c));
 #pragma unroll
-        for (int k = 0; k < NU; ++k) conv_unit(k, &ER[0][0], s0, z0);
+        for (int k = 0; k < NU; ++k) conv_unit(k, &IMG[0][0], s0, z0);
+        const Tile t1 = tile_of(clampt(blockIdx.x + G));
+        set_load_tile(t1);
+#pragma unroll
+        for (int k = 0; k < NU; ++k) load_unit(t1, k);
     }
 
     STAMP(13)
-    // one tile; FIRST (the peeled first tile) has no pending epilogue 2.  Peeling keeps the
-    // sequence of vector-memory operations identical in every loop iteration, so the compiler's
-    // counted waits for the row loads never include the epilogue's stores.
     auto tile_body = [&](auto first_tag, int tile, int it) {
         constexpr bool FIRST = decltype(first_tag)::value;
         const Tile cu = tile_of(tile);
         const Tile nt = tile_of(clampt(tile + G));
-                // T: the image of this tile complete (converted during the previous phase D)
-        lds_barrier();
+        const Tile n2 = tile_of(clampt(tile + 2 * G));
+        set_load_tile(n2);   // (tile i+1's loads were all issued in the previous tile)
+        lds_barrier();       // T: image i complete (converted in the previous tile's A / B)
         STAMP(0)
         const float gm = gm_c;
         const int m_e = scale_exp(gm);
@@ -369,60 +352,60 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         const uint32_t zn = zero_bits_of(nt);
         const float sv = exp2i(m_v);
         a1 = exp2i(m_v - m_e - a.kd);
-        if (sv != bs_sv) {   // the clip's v scale changed: b_d 2^m_v of this wave's channels (only
-            bs_sv = sv;      // this wave reads them, in program order after these writes)
+        if (sv != bs_sv) {
+            bs_sv = sv;
             if (lane < 32) BDS[32 * w + lane] = BIAS[32 * w + lane] * sv;
         }
-        uint8_t* erp = &ER[(it & 1) ^ 1][0];   // the previous tile's residual, then the next's
+        const uint8_t* imc = &IMG[it & 1][0];
+        uint8_t* imn = &IMG[(it & 1) ^ 1][0];
 
         STAMP(10)
-        // A: GEMM 1 half 0 + epilogue 2 of the previous tile
+        // A: GEMM 1 half 0 + this tile's residual rows (loads) + epilogue 2 of the previous tile
+        //    and the flush of its half 0 + conversion units 0..4 (each unit's registers reloaded
+        //    with tile i+2 right away)
+        if (!FIRST) epi2_begin();
+        gemm1h(J0{}, [&](int st) {
+            if (st < 2) {   // (issued before this tile's row loads: their waits do not include those)
+#pragma unroll
+                for (int p = 0; p < 4; ++p) rr_load(cu, 4 * st + p);
+            }
+            if (!FIRST) {
+                epi2_part(st / 3, st % 3);
+                if (st >= 12 && st < 20) flush_part(0, (st - 12) >> 1, st & 1);
+            }
+            if (st % 5 == 2) {   // steps 2 7 12 17 22: units 0..4
+                conv_unit(st / 5, imn, s_next, zn);
+                load_unit(n2, st / 5);
+            }
+        }, cu, imc);
         if (!FIRST) {
-            epi2_begin();
-#if defined(SW_EXP) && SW_EXP == 10
-            gemm1h(J0{}, [&](int) {}, cu);
-#else
-            gemm1h(J0{}, [&](int st) {
-                epi2_part(st / 3, st % 3, erp);
-                if (st >= 12 && st < 20) flush_part(0, (st - 12) >> 1, st & 1, erp);
-                if (st % 3 == 1 && st < 15) load_unit(nt, st / 3);   // rows of tile i+1: units 0..4
-            }, cu);
-#endif
             epi2_words();
             if (cu.b != prv.b) epi2_max();
-        } else {
-            gemm1h(J0{}, [&](int st) { if (st % 3 == 1 && st < 15) load_unit(nt, st / 3); }, cu);
         }
         STAMP(5)
-        // B: GEMM 1 half 1 + epilogue 1 of half 0
-#if defined(SW_EXP) && SW_EXP == 10
-        gemm1h(J1{}, [&](int) {}, cu);
-#pragma unroll
-        for (int st = 0; st < 8; ++st) epi1_part(0, st >> 1, st & 1);
-#else
+        // B: GEMM 1 half 1 + epilogue 1 of half 0 + the flush of epilogue 2's half 1 +
+        //    conversion units 5..8
         gemm1h(J1{}, [&](int st) {
             if (st < 8) epi1_part(0, st >> 1, st & 1);
-            else if (!FIRST && st < 16) flush_part(1, (st - 8) >> 1, st & 1, erp);
-            if (st >= 11 && st % 3 == 2) load_unit(nt, 5 + (st - 11) / 3);   // units 5..8: 11 14 17 20
-        }, cu);
-#endif
+            else if (!FIRST && st < 16) flush_part(1, (st - 8) >> 1, st & 1);
+            if (st >= 9 && st % 4 == 1) {   // steps 9 13 17 21: units 5..8
+                conv_unit(5 + (st - 9) / 4, imn, s_next, zn);
+                load_unit(n2, 5 + (st - 9) / 4);
+            }
+        }, cu, imc);
         lds_barrier();   // v image half 0, u > 0 words half 0, e > 0 words of tile i-1
         STAMP(1)
         if (!FIRST) store_me(prv.b);
         // C: GEMM 2 half 0 + epilogue 1 of half 1
-        gemm2h(J0{}, [&](int kb) {
-            epi1_part(1, kb >> 1, kb & 1);
-        });
+        gemm2h(J0{}, [&](int kb) { epi1_part(1, kb >> 1, kb & 1); });
         lds_barrier();   // v image half 1, all u > 0 words
         STAMP(2)
-        if (lane < 16)   // u > 0 words of the tile (this layer's positions): wave w, columns 16 w..
+        if (lane < 16)
             *reinterpret_cast<uint4*>(a.mu + ((size_t)cu.b * a.T + cu.p0 + 16 * w + lane) * 8) =
                 *reinterpret_cast<const uint4*>(&MBU[(16 * w + lane) * 8]);
-        // D: GEMM 2 half 1 + conversion of tile i+1, each unit's registers reloaded with i+2
-        gemm2h(J1{}, [&](int kb) {
-            conv_unit(kb, erp, s_next, zn);
-            if (kb == 7) conv_unit(NU - 1, erp, s_next, zn);
-        });
+        // D: GEMM 2 half 1 + this tile's residual rows into the staging rows (the flush of the
+        //    previous tile's rows ended in B)
+        gemm2h(J1{}, [&](int kb) { rr_write(kb); });
         STAMP(3)
         prv = cu;
         inv2p = exp2i(-(m_v + a.kr));
@@ -433,14 +416,13 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         tile_body(std::false_type{}, tile, it);
     // drain: epilogue 2 of the last tile
     {
-        uint8_t* erl = &ER[(it - 1) & 1][0];
         epi2_begin();
 #pragma unroll
-        for (int st = 0; st < 24; ++st) epi2_part(st / 3, st % 3, erl);
+        for (int st = 0; st < 24; ++st) epi2_part(st / 3, st % 3);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            flush_part(q >> 2, q & 3, 0, erl);
-            flush_part(q >> 2, q & 3, 1, erl);
+            flush_part(q >> 2, q & 3, 0);
+            flush_part(q >> 2, q & 3, 1);
         }
         epi2_words();
         epi2_max();
@@ -453,27 +435,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
 
 }  // namespace
 
-bool launch_block_fwd_roles(const FwdArgsS& a, hipStream_t s);   // block_fwd_roles.hip
-bool launch_block_fwd_db(const FwdArgsS& a, hipStream_t s);      // block_fwd_db.hip
-
-// ASTYLE_FWD_ROLES=1 selects the role-split kernel (block_fwd_roles.hip, bit-identical results;
-// measured 3-4 % slower than this one-wave-per-SIMD kernel)
-static bool fwd_roles() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("ASTYLE_FWD_ROLES"); v = e ? (atoi(e) != 0) : 0; }
-    return v != 0;
-}
-
-// ASTYLE_FWD_DB=1 selects the double-buffered-image kernel (block_fwd_db.hip, bit-identical)
-static bool fwd_db() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("ASTYLE_FWD_DB"); v = e ? (atoi(e) != 0) : 0; }
-    return v != 0;
-}
-
-void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
-    if (fwd_roles()) { launch_block_fwd_roles(a0, s); return; }
-    if (fwd_db()) { launch_block_fwd_db(a0, s); return; }
+bool launch_block_fwd_db(const FwdArgsS& a0, hipStream_t s) {
     FwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
     a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));
@@ -481,20 +443,10 @@ void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
     const dim3 grid(std::min(nt, sw::num_cus()));
     Layout ly;
     const bool masked = pick_layout(a.n, ly);
-    if (masked) hipLaunchKernelGGL((k_block_fwd_s<true, false>), grid, dim3(FT), 0, s, a, ly);
-    else if (ly.M == TMS) hipLaunchKernelGGL((k_block_fwd_s<false, true>), grid, dim3(FT), 0, s, a, ly);
-    else hipLaunchKernelGGL((k_block_fwd_s<false, false>), grid, dim3(FT), 0, s, a, ly);
-}
-
-int sw::num_cus() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus <= 0) cus = 256;
-    }
-    return cus;
+    if (masked) hipLaunchKernelGGL((k_block_fwd_db<true, false>), grid, dim3(FT), 0, s, a, ly);
+    else if (ly.M == TMS) hipLaunchKernelGGL((k_block_fwd_db<false, true>), grid, dim3(FT), 0, s, a, ly);
+    else hipLaunchKernelGGL((k_block_fwd_db<false, false>), grid, dim3(FT), 0, s, a, ly);
+    return true;
 }
 
 }  // namespace ast

@@ -1,8 +1,9 @@
-"""The role-split forward block kernel (block_fwd_roles.hip, ASTYLE_FWD_ROLES=1) against the
-default one-wave kernel: the same split numerics, so every extract must be bit-identical, on every
+"""The alternative split forward block kernels against the default one-wave kernel: the
+role-split kernel (block_fwd_roles.hip, ASTYLE_FWD_ROLES=1) and the double-buffered-image kernel
+(block_fwd_db.hip, ASTYLE_FWD_DB=1).  Same split numerics, so every extract must be bit-identical, on every
 dilation layout (T = 3584: one segment with halo rows, per-column tap masks where 64-position tiles
 start and end inside sub-sequences; T = 2048: the 32-position two-segment layout) and with several
-clips per launch.  The knob is read once per process, so the role-split run is a child process
+clips per launch.  The knob is read once per process, so each run is a child process
 (the engine is built after the environment is set)."""
 import json
 import os
@@ -36,20 +37,23 @@ np.savez(out, **{'e%d' % i: eng.extract(i).cpu().numpy() for i in ids})
 '''
 
 
-def _run(B, T, roles, path):
-    env = dict(os.environ, ASTYLE_FWD_ROLES='1' if roles else '0')
+def _run(B, T, knob, path):
+    env = dict(os.environ, ASTYLE_FWD_ROLES='0', ASTYLE_FWD_DB='0')
+    if knob:
+        env[knob] = '1'
     subprocess.run([sys.executable, '-c', CHILD, ROOT, str(B), str(T), path, json.dumps(IDS)],
                    env=env, check=True, timeout=240)
     with np.load(path) as z:
         return {k: z[k] for k in z.files}
 
 
-@pytest.mark.parametrize('B,T', [(3, 3584), (2, 2048)])
-def test_roles_forward_bit_identical(B, T):
+@pytest.mark.parametrize('knob', ['ASTYLE_FWD_ROLES', 'ASTYLE_FWD_DB'])
+@pytest.mark.parametrize('B,T', [(3, 3584), (2, 2048), (2, 512)])
+def test_alt_forward_bit_identical(B, T, knob):
     assert torch.cuda.is_available(), 'gpu tests need an MI355X'
     with tempfile.TemporaryDirectory() as d:
-        ref = _run(B, T, False, os.path.join(d, 'one.npz'))
-        got = _run(B, T, True, os.path.join(d, 'roles.npz'))
+        ref = _run(B, T, None, os.path.join(d, 'one.npz'))
+        got = _run(B, T, knob, os.path.join(d, 'alt.npz'))
     for k in ref:
         assert np.isfinite(ref[k]).all()
         assert np.array_equal(ref[k], got[k]), (k, float(np.abs(ref[k] - got[k]).max()))
