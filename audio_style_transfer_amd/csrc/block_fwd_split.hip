@@ -265,6 +265,18 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         }
     };
 
+
+#if defined(SW_EXP) && (SW_EXP == 35 || SW_EXP == 36)
+    // (timing experiment: 4 / 8 plain fp32 FMAs per GEMM step on independent chains, no inline asm,
+    //  so the scheduler places them like the kernels' own VALU)
+    float ff[8] = {1.f, 2.f, 3.f, 4.f, 5.f, 6.f, 7.f, 8.f};
+    auto filler = [&]() {
+#pragma unroll
+        for (int q = 0; q < (SW_EXP == 35 ? 4 : 8); ++q) ff[q] = fmaf(ff[q], 1.0001f, 0.5f);
+    };
+#else
+    auto filler = [&]() {};
+#endif
     // ---- GEMM 1 of column half J over the image; side work per step ----
     auto gemm1h = [&](auto j_tag, auto side, const Tile& cu) {
         constexpr int J = decltype(j_tag)::value;
@@ -299,6 +311,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             acc1[J] = mfma_f16(wd[tp][kb][0], xh, acc1[J]);
             if (st + LA < 24) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
             side(st);
+            filler();
 #if !(defined(SW_EXP) && SW_EXP == 20)   // (timing experiment: drop the w_lo products)
             acc1[J] = mfma_f16(wd[tp][kb][1], xh, acc1[J]);
 #endif
@@ -325,6 +338,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             acc2[J] = mfma_f16(wr[kb][0], bh[cb], acc2[J]);
             if (kb + LA < 8) bload(kb + LA, bh[(kb + LA) % (LA + 1)], bl[(kb + LA) % (LA + 1)]);
             side(kb);
+            filler();
 #if !(defined(SW_EXP) && SW_EXP == 20)
             acc2[J] = mfma_f16(wr[kb][1], bh[cb], acc2[J]);
 #endif
@@ -447,6 +461,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         lds_barrier();
         store_me(prv.b);
     }
+#if defined(SW_EXP) && (SW_EXP == 35 || SW_EXP == 36)
+    if (ff[0] + ff[1] + ff[2] + ff[3] + ff[4] + ff[5] + ff[6] + ff[7] == 1.5f) a.gmax_out[0] = 0u;   // (keeps the filler live)
+#endif
     STAMP(4)
     STAMP_FLUSH(a.stamps)
 }
