@@ -23,6 +23,8 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall',
 # unrolled tile loops exceed the default pragma-unroll size limit (a partly unrolled loop would
 # index the register-resident weight arrays dynamically and demote them to scratch)
 _CW = ['-mllvm', '-amdgpu-mfma-vgpr-form=1', '-mllvm', '-amdgpu-atomic-optimizer-strategy=None', '-mllvm', '-pragma-unroll-threshold=1000000', '-fno-slp-vectorize']
+if os.environ.get('ASTYLE_NO_VGPR_FORM'):   # A/B builds: let the compiler place MFMA accumulators (AGPRs)
+    _CW = _CW[2:]
 EXTRA = {'block_fwd_bf16.hip': _CW, 'block_bwd_bf16.hip': _CW, 'block_fwd_split.hip': _CW,
          'block_bwd_split.hip': _CW, 'block_fwd_roles.hip': _CW, 'block_fwd_db.hip': _CW}
 
