@@ -11,8 +11,13 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, 'csrc')
 LIB = os.path.join(PKG, 'libastyle.so')
 SOURCES = ['encoder.hip', 'block_fwd_bf16.hip', 'block_bwd_bf16.hip', 'block_fwd_split.hip',
-           'block_bwd_split.hip', 'block_fwd_roles.hip', 'block_fwd_db.hip', 'gram.hip', 'gram_bf16.hip', 'gram_split.hip', 'gram_gatys.hip', 'stft_reg.hip',
-           'lbfgs.hip', 'ot_admm.hip', 'api.hip', 'ckpt.cpp']
+           'block_bwd_split.hip', 'gram.hip', 'gram_bf16.hip', 'gram_split.hip', 'gram_gatys.hip',
+           'stft_reg.hip', 'lbfgs.hip', 'ot_admm.hip', 'api.hip', 'ckpt.cpp']
+# tools-only A/B build (ASTYLE_VARIANT=fwdvariants -> libastyle_fwdvariants.so): the measured-
+# slower forward block kernels of round 3, selected at run time by
+# ASTYLE_FWD_ROLES=1 / ASTYLE_FWD_DB=1; never part of the shipped libastyle.so
+VARIANTS = os.path.join(os.path.dirname(PKG), 'tools', 'variants')
+VARIANT_SOURCES = {'fwdvariants': (['block_fwd_roles.hip', 'block_fwd_db.hip'], ['-DASTYLE_FWD_VARIANTS'])}
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 CXX = os.environ.get('CXX', 'g++')          # host-only sources (.cpp)
 CXXFLAGS = ['-O2', '-fPIC', '-std=c++17', '-Wall']
@@ -38,28 +43,33 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, stamps: bool = False, exp: int = 0) -> str:
-    """exp > 0 (stamps builds): -DSW_EXP=exp, a timing experiment of the split block kernels
-    (drops parts of their work; results are wrong) -> libastyle_stamps_exp<exp>.so"""
-    tag = '' if not exp else '_exp%d' % exp
-    lib = LIB if not stamps else os.path.join(PKG, 'libastyle_stamps%s.so' % tag)
+def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:
+    """The shipped libastyle.so; stamps=True: the phase-stamp diagnostic build
+    (libastyle_stamps.so, tools/stamps.py).  ASTYLE_VARIANT=<name> (+ ASTYLE_DEFS): an A/B build
+    libastyle_<name>.so, with the tools/variants sources of VARIANT_SOURCES[name] if any."""
+    lib = LIB if not stamps else os.path.join(PKG, 'libastyle_stamps.so')
     variant = os.environ.get('ASTYLE_VARIANT', '')   # A/B builds: libastyle_<variant>.so
     defs = os.environ.get('ASTYLE_DEFS', '').split()
+    sources = list(SOURCES)
     if variant:
         lib = os.path.join(PKG, 'libastyle_%s.so' % variant)
-        stamps = stamps or False
+        extra_src, extra_defs = VARIANT_SOURCES.get(variant, ([], []))
+        sources += [os.path.join(VARIANTS, f) for f in extra_src]
+        defs += extra_defs
     if not force and not stamps and not variant and not _stale():
         return LIB
-    objdir = os.path.join(PKG, 'build_' + variant if variant else 'build' if not stamps else 'build_stamps' + tag)
-    flags = FLAGS + (['-DASTYLE_STAMPS'] if stamps else []) + (['-DSW_EXP=%d' % exp] if exp else []) + defs
+    objdir = os.path.join(PKG, 'build_' + variant if variant else 'build' if not stamps else 'build_stamps')
+    flags = FLAGS + (['-DASTYLE_STAMPS'] if stamps else []) + defs
     os.makedirs(objdir, exist_ok=True)
 
     def cc(src):
-        obj = os.path.join(objdir, src.rsplit('.', 1)[0] + '.o')
+        name = os.path.basename(src)
+        obj = os.path.join(objdir, name.rsplit('.', 1)[0] + '.o')
+        path = src if os.path.isabs(src) else os.path.join(CSRC, src)
         if src.endswith('.cpp'):
-            cmd = [CXX, *CXXFLAGS, '-c', os.path.join(CSRC, src), '-o', obj]
+            cmd = [CXX, *CXXFLAGS, '-c', path, '-o', obj]
         else:
-            cmd = [HIPCC, *flags, *EXTRA.get(src, []), '-c', os.path.join(CSRC, src), '-o', obj]
+            cmd = [HIPCC, *flags, '-I', CSRC, *EXTRA.get(name, []), '-c', path, '-o', obj]
         if verbose:
             print(' '.join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -69,8 +79,8 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, exp:
             print(r.stderr, file=sys.stderr)
         return obj
 
-    with ThreadPoolExecutor(len(SOURCES)) as ex:
-        objs = list(ex.map(cc, SOURCES))
+    with ThreadPoolExecutor(len(sources)) as ex:
+        objs = list(ex.map(cc, sources))
     tmp = lib + '.tmp'
     cmd = [HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', *objs, '-o', tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -81,6 +91,4 @@ def build(force: bool = False, verbose: bool = False, stamps: bool = False, exp:
 
 
 if __name__ == '__main__':
-    exp = int(sys.argv[sys.argv.index('--exp') + 1]) if '--exp' in sys.argv else 0
-    print(build(force='--force' in sys.argv, verbose=True, stamps='--stamps' in sys.argv or exp > 0,
-                exp=exp))
+    print(build(force='--force' in sys.argv, verbose=True, stamps='--stamps' in sys.argv))

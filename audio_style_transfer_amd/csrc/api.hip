@@ -128,7 +128,7 @@ struct ast_ctx {
     float* stft_gfr = nullptr;              //   per-frame gradients [B][nf][1024]
     std::vector<const void*> lb_ws;         // workspaces started here with x0 (ast_lbfgs_begin)
     void* zero = nullptr;                   // 256 zero bytes
-    int* rflags = nullptr;                  // [B] AST_RANGE_* of the last ast_loss_grad
+    int* rflags = nullptr;                  // [B] AST_RANGE_* OR'ed over ast_loss_grad calls since the last reset
     size_t gpart_elems = 0, smat_elems = 0; // per context (mode-dependent)
     int ncpart = 0;
     std::vector<void*> allocs;
@@ -988,6 +988,12 @@ int ast_range_flags(ast_ctx* x, int* flags, void* stream) {
     return 0;
 }
 
+int ast_range_flags_reset(ast_ctx* x, void* stream) {
+    if (!x) return fail(AST_E_ARG, "null argument");
+    HIPCHK(hipMemsetAsync(x->rflags, 0, (size_t)x->cfg.batch * 4, S(stream)));
+    return 0;
+}
+
 int ast_adam_step(ast_ctx* x, float* xd, float* m, float* v, const float* grad, int step,
                   float lr, float b1, float b2, float eps, void* stream) {
     if (!x || !xd || !m || !v || !grad || step < 1) return fail(AST_E_ARG, "bad argument");
@@ -1021,6 +1027,8 @@ int ast_lbfgs_begin(ast_ctx* x, void* ws, float* xd, const double* x0, const int
     if (!x0 && !known)
         return fail(AST_E_STATE, "continuing (x0 NULL) needs a workspace started with x0");
     if (x0 && !known) x->lb_ws.push_back(ws);
+    // a new epoch: the range flags accumulate over its evaluations (include/astyle.h)
+    HIPCHK(hipMemsetAsync(x->rflags, 0, (size_t)x->cfg.batch * 4, S(stream)));
     launch_lbfgs_begin(ws, xd, x0, active, x->cfg.batch, x->cfg.T, m, maxiter, maxls, ftol, gtol,
                        S(stream));
     HIPCHK(hipGetLastError());

@@ -256,10 +256,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             oo.y = fmaf(keep_if(acc2[J][4 * g + 1], mw, 4 + g), inv2, oe.y);
             oo.z = fmaf(keep_if(acc2[J][4 * g + 2], mw, 8 + g), inv2, oe.z);
             oo.w = fmaf(keep_if(acc2[J][4 * g + 3], mw, 12 + g), inv2, oe.w);
-#if !(defined(SW_EXP) && SW_EXP == 8)
             if (MASKED) *reinterpret_cast<float4*>(dst + 8 * g) = oo;
             else bst4(rs_o, ocol + 32 * g, 0u, oo);
-#endif
         } else {
             omax = fmaxf(omax, fmaxf(fmaxf(fabsf(oo.x), fabsf(oo.y)), fmaxf(fabsf(oo.z), fabsf(oo.w))));
         }
@@ -360,9 +358,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             for (int k = 0; k < NU; ++k)
                 if (st == (24 * k) / NU) {
                     conv_unit(k, ero, s_next, zn);
-#if !(defined(SW_EXP) && SW_EXP == 9)
                     load_unit(n2, k);
-#endif
                 }
             if (st == 3) load_masks(nt, mu_n, muh_n, me_n);
         }, cu);

@@ -266,17 +266,6 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     };
 
 
-#if defined(SW_EXP) && (SW_EXP == 35 || SW_EXP == 36)
-    // (timing experiment: 4 / 8 plain fp32 FMAs per GEMM step on independent chains, no inline asm,
-    //  so the scheduler places them like the kernels' own VALU)
-    float ff[8] = {1.f, 2.f, 3.f, 4.f, 5.f, 6.f, 7.f, 8.f};
-    auto filler = [&]() {
-#pragma unroll
-        for (int q = 0; q < (SW_EXP == 35 ? 4 : 8); ++q) ff[q] = fmaf(ff[q], 1.0001f, 0.5f);
-    };
-#else
-    auto filler = [&]() {};
-#endif
     // ---- GEMM 1 of column half J over the image; side work per step ----
     auto gemm1h = [&](auto j_tag, auto side, const Tile& cu) {
         constexpr int J = decltype(j_tag)::value;
@@ -311,10 +300,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             acc1[J] = mfma_f16(wd[tp][kb][0], xh, acc1[J]);
             if (st + LA < 24) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
             side(st);
-            filler();
-#if !(defined(SW_EXP) && SW_EXP == 20)   // (timing experiment: drop the w_lo products)
             acc1[J] = mfma_f16(wd[tp][kb][1], xh, acc1[J]);
-#endif
             acc1[J] = mfma_f16(wd[tp][kb][0], xl, acc1[J]);
             step3_schedule();
         }
@@ -338,10 +324,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
             acc2[J] = mfma_f16(wr[kb][0], bh[cb], acc2[J]);
             if (kb + LA < 8) bload(kb + LA, bh[(kb + LA) % (LA + 1)], bl[(kb + LA) % (LA + 1)]);
             side(kb);
-            filler();
-#if !(defined(SW_EXP) && SW_EXP == 20)
             acc2[J] = mfma_f16(wr[kb][1], bh[cb], acc2[J]);
-#endif
             acc2[J] = mfma_f16(wr[kb][0], bl[cb], acc2[J]);
             step3_schedule();
         }
@@ -393,15 +376,11 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         // A: GEMM 1 half 0 + epilogue 2 of the previous tile
         if (!FIRST) {
             epi2_begin();
-#if defined(SW_EXP) && SW_EXP == 10
-            gemm1h(J0{}, [&](int) {}, cu);
-#else
             gemm1h(J0{}, [&](int st) {
                 epi2_part(st / 3, st % 3, erp);
                 if (st >= 12 && st < 20) flush_part(0, (st - 12) >> 1, st & 1, erp);
                 if (st % 3 == 1 && st < 15) load_unit(nt, st / 3);   // rows of tile i+1: units 0..4
             }, cu);
-#endif
             epi2_words();
             if (cu.b != prv.b) epi2_max();
         } else {
@@ -409,17 +388,11 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         }
         STAMP(5)
         // B: GEMM 1 half 1 + epilogue 1 of half 0
-#if defined(SW_EXP) && SW_EXP == 10
-        gemm1h(J1{}, [&](int) {}, cu);
-#pragma unroll
-        for (int st = 0; st < 8; ++st) epi1_part(0, st >> 1, st & 1);
-#else
         gemm1h(J1{}, [&](int st) {
             if (st < 8) epi1_part(0, st >> 1, st & 1);
             else if (!FIRST && st < 16) flush_part(1, (st - 8) >> 1, st & 1, erp);
             if (st >= 11 && st % 3 == 2) load_unit(nt, 5 + (st - 11) / 3);   // units 5..8: 11 14 17 20
         }, cu);
-#endif
         lds_barrier();   // v image half 0, u > 0 words half 0, e > 0 words of tile i-1
         STAMP(1)
         if (!FIRST) store_me(prv.b);
@@ -461,36 +434,25 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         lds_barrier();
         store_me(prv.b);
     }
-#if defined(SW_EXP) && (SW_EXP == 35 || SW_EXP == 36)
-    if (ff[0] + ff[1] + ff[2] + ff[3] + ff[4] + ff[5] + ff[6] + ff[7] == 1.5f) a.gmax_out[0] = 0u;   // (keeps the filler live)
-#endif
     STAMP(4)
     STAMP_FLUSH(a.stamps)
 }
 
 }  // namespace
 
-bool launch_block_fwd_roles(const FwdArgsS& a, hipStream_t s);   // block_fwd_roles.hip
-bool launch_block_fwd_db(const FwdArgsS& a, hipStream_t s);      // block_fwd_db.hip
-
-// ASTYLE_FWD_ROLES=1 selects the role-split kernel (block_fwd_roles.hip, bit-identical results;
-// measured 3-4 % slower than this one-wave-per-SIMD kernel)
-static bool fwd_roles() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("ASTYLE_FWD_ROLES"); v = e ? (atoi(e) != 0) : 0; }
-    return v != 0;
-}
-
-// ASTYLE_FWD_DB=1 selects the double-buffered-image kernel (block_fwd_db.hip, bit-identical)
-static bool fwd_db() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("ASTYLE_FWD_DB"); v = e ? (atoi(e) != 0) : 0; }
-    return v != 0;
-}
+#ifdef ASTYLE_FWD_VARIANTS
+// tools/variants/ build only (libastyle_fwdvariants.so): the measured-slower alternatives of this
+// kernel, bit-identical, selected by ASTYLE_FWD_ROLES=1 / ASTYLE_FWD_DB=1
+bool launch_block_fwd_roles(const FwdArgsS& a, hipStream_t s);   // tools/variants/block_fwd_roles.hip
+bool launch_block_fwd_db(const FwdArgsS& a, hipStream_t s);      // tools/variants/block_fwd_db.hip
+static bool env_on(const char* k) { const char* e = getenv(k); return e && atoi(e) != 0; }
+#endif
 
 void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
-    if (fwd_roles()) { launch_block_fwd_roles(a0, s); return; }
-    if (fwd_db()) { launch_block_fwd_db(a0, s); return; }
+#ifdef ASTYLE_FWD_VARIANTS
+    if (env_on("ASTYLE_FWD_ROLES")) { launch_block_fwd_roles(a0, s); return; }
+    if (env_on("ASTYLE_FWD_DB")) { launch_block_fwd_db(a0, s); return; }
+#endif
     FwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
     a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));

@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(256) k_finalize(float* parts, const float* cpa
     }
 }
 
-// Per-clip flags (include/astyle.h AST_RANGE_*): non-finite loss parts or gradient; in split
+// Per-clip flags (include/astyle.h AST_RANGE_*), OR'ed into the context's accumulated flags: non-finite loss parts or gradient; in split
 // mode also every per-clip maximum the split-fp16 scales were derived from (splitwave.h
 // scale_exp: in range for maxima in [2^-47, 2^74)) and the analytic intermediate bounds
 // |u| <= wdn max|e_l| + bdm, |W_r tot| <= wrn max|tot|: beyond 2^74 the scaled halves would
@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(256) k_range_flags(RangeArgs a) {
             }
         }
     }
-    a.flags[b] = f;
+    a.flags[b] |= f;   // sticky until ast_range_flags_reset / ast_lbfgs_begin
 }
 
 void launch_range_flags(const RangeArgs& a, hipStream_t s) {

@@ -190,10 +190,13 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
         for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (lrs[k] ? lofs + (uint32_t)(t0 + st) * C : 0u));
     };
     auto stage = [&](float4 (&v)[8], int t0) {
-        float4 ce, cph;
+        float4 ce, cph = make_float4(0.f, 0.f, 0.f, 0.f);
         if (CONT && cthr) {
             ce = *reinterpret_cast<const float4*>(ce_src + (size_t)(t0 + ctt) * C);
-            cph = *reinterpret_cast<const float4*>(cp_src + (size_t)(t0 + ctt) * a.cont_ncc);
+            // phi rows hold only the tap's cont_ncol (a multiple of 4) channels: quads past them
+            // load nothing (the row's last quad can end the caller's buffer)
+            if (c0 + 4 * cq < a.cont_ncol)
+                cph = *reinterpret_cast<const float4*>(cp_src + (size_t)(t0 + ctt) * a.cont_ncc);
         }
         uint4 fh[4], fl[4];   // channel 4 sq + j: tensors 8 uo .. + 8 at row st, hi / lo
         split8<0>(v, fh[0], fl[0]);

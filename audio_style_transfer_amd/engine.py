@@ -191,13 +191,20 @@ class StyleEngine:
                                               float(beta1), float(beta2), float(eps),
                                               self._stream()))
 
-    def range_flags(self) -> torch.Tensor:
-        """Per-clip AST_RANGE_* flags [B] (int32, device) of the last loss_grad: non-finite
-        loss parts or gradient (1); in split mode a per-clip maximum or analytic operand bound
-        outside the split-fp16 range (2: forward, 4: backward) or below 2^-60 (8)."""
+    def range_flags(self, reset: bool = False) -> torch.Tensor:
+        """Per-clip AST_RANGE_* flags [B] (int32, device), OR'ed over every loss_grad since the
+        last reset (reset_range_flags, LbfgsLoop.begin, AdamLoop start, context creation):
+        non-finite loss parts or gradient (1); in split mode a per-clip maximum or analytic
+        operand bound outside the split-fp16 range (2: forward, 4: backward) or below 2^-60 (8).
+        ``reset=True`` clears them after reading."""
         out = torch.empty(self.batch, dtype=torch.int32, device=self.device)
         _lib.check(self.lib.ast_range_flags(self.h, self._ptr(out, torch.int32), self._stream()))
+        if reset:
+            self.reset_range_flags()
         return out
+
+    def reset_range_flags(self) -> None:
+        _lib.check(self.lib.ast_range_flags_reset(self.h, self._stream()))
 
     @staticmethod
     def nonfinite_clips(parts: torch.Tensor, grad: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -238,6 +245,7 @@ class AdamLoop:
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=x.device)
         self.hp = (float(lr), float(beta1), float(beta2), float(eps))
         self.graph = None
+        eng.reset_range_flags()   # range_flags() then covers every step of this loop
         if graph:
             self._capture()
 
@@ -254,6 +262,7 @@ class AdamLoop:
             self._eager()
         for t, s in zip((self.x, self.m, self.v, self.step_dev), saved):
             t.copy_(s)
+        self.eng.reset_range_flags()   # (the warm-up step is not one of the loop's steps)
         self.graph = g
         self._gen = self.eng.gen
 

@@ -84,11 +84,11 @@ class GatysNet(object):
         self.engine = self.build(batch_size)
         self.embeds_shape = self.engine.style_shape
 
-    def build(self, length, batch=1, lambd=100.0):
+    def build(self, length, batch=1, lambd=100.0, precision=None):
         """methods.py:44-77: encoder + taps + Gram + l2norm, here one libastyle context."""
         return StyleEngine(batch, length, self.cont_lyr_ids, self.style_lyr_ids,
                            cnt_channels=self.cnt_channels, nb_channels=self.nb_channels,
-                           gatys=self.gatys, lambd=lambd, precision=self.precision,
+                           gatys=self.gatys, lambd=lambd, precision=precision or self.precision,
                            device=self.device, weights=self.weights)
 
     def get_embeds(self, *args, is_content=True):
@@ -175,6 +175,8 @@ class GatysNet(object):
         def fg(v):
             nonlocal eng
             xd.copy_(torch.from_numpy(v.astype(np.float32)).view(1, T))
+            if eng.precision == 'split':
+                eng.reset_range_flags()                                   # this evaluation's flags
             parts, grad = eng.loss_grad(xd)                               # incl. gamma * reg
             if eng.precision == 'split' and self._split_out_of_range(eng, log):
                 eng = self._fp32_engine(phi_c, phi_s, lambd, gamma)
@@ -202,6 +204,8 @@ class GatysNet(object):
             else:
                 info = loop.minimize(torch.tensor(x[None], dtype=torch.float64)
                                      if ep == start_ep else None)
+                # the flags are sticky over the epoch (begin resets them): any out-of-range
+                # evaluation, line-search trials included, sends the epoch to the fp32 kernels
                 if eng.precision == 'split' and self._split_out_of_range(eng, log):
                     # redo the epoch from its start point x with the fp32 kernels
                     eng = self._fp32_engine(phi_c, phi_s, lambd, gamma)
@@ -228,11 +232,14 @@ class GatysNet(object):
             if state['i_'] < 50:                                          # methods.py:180-181
                 break
         writer.close()
+        if eng is not self.engine:   # the range guard's fp32 context
+            eng.close()
         self.history = history
         return x
 
     def _split_out_of_range(self, eng, log) -> bool:
-        """After a split-precision evaluation: AST_RANGE_* flags of the clip (engine.range_flags).
+        """After split-precision evaluations: AST_RANGE_* flags of the clip accumulated since the
+        last reset (engine.range_flags: one evaluation on the scipy path, a whole device epoch).
         Non-finite results or operands outside the split-fp16 range (flags 1, 2, 4) -> True (the
         caller switches to the fp32 kernels); operands below 2^-60 (8) only lose low-order bits
         and are reported once."""
@@ -247,12 +254,13 @@ class GatysNet(object):
         return bool(bad)
 
     def _fp32_engine(self, phi_c, phi_s, lambd, gamma):
-        self.precision = 'fp32'
-        new = self.build(self.batch_size, lambd=lambd)
+        """The range guard's fallback for the rest of this l_bfgs call: an fp32-kernel context
+        of its own (self.precision, self.engine and the resume fingerprint stay as chosen; the
+        context is closed when l_bfgs returns)."""
+        new = self.build(self.batch_size, lambd=lambd, precision='fp32')
         new.set_targets(torch.as_tensor(phi_c, dtype=torch.float32),
                         torch.as_tensor(phi_s, dtype=torch.float32))
         new.set_gamma(gamma)
-        self.engine = new
         return new
 
     def _run_fingerprint(self, phi_c, phi_s, lambd, gamma, optimizer):
@@ -343,7 +351,8 @@ def make_parser():
     parser.add_argument('--precision', default='split', choices=['fp32', 'split', 'bf16'],
                         help='split (default): fp32 storage, split-fp16 MFMA with fp32 '
                              'accumulation (gradient within 2e-4 rel-L2 of fp64, range-checked '
-                             'per clip: ast_range_flags); fp32: plain fp32 FMA kernels; bf16: '
+                             'per clip: ast_range_flags); fp32: fp32 storage + fp32 MFMA '
+                             '(v_mfma_f32_32x32x2_f32, also the range guard\'s fallback); bf16: '
                              'bf16 storage + bf16 MFMA')
     parser.add_argument('--weights', default=None, help='npz of TF-named encoder weights')
     parser.add_argument('--no_plots', action='store_true', help='skip the Gram PNGs')

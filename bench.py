@@ -186,8 +186,12 @@ def run(args, Eng, precision, steps, warmup, ws, rank, dev, graph, clips=None, g
     el = time.perf_counter() - t0
     el = max_over_ranks(el, ws, device=dev)
     last_loss = loop.parts[:, 0].mean().item()
-    # per-clip flag: the clip's loss parts or gradient hold a NaN / Inf
+    # per-clip flag: the clip's loss parts or gradient hold a NaN / Inf (last step), and the
+    # clips whose range flags (sticky over every warm-up and timed step: AdamLoop resets them
+    # at its start) report an out-of-range or non-finite evaluation
     bad = int((~torch.isfinite(loop.parts).all(dim=1) | ~torch.isfinite(loop.grad).all(dim=1)).sum().item())
+    flagged = int((eng.range_flags() & 7).ne(0).sum().item()) if dev.type == 'cuda' else 0
+    bad = (bad, flagged)
     eng.timing(True)
     for _ in range(2):
         loop._eager()
@@ -441,7 +445,8 @@ def rank_main(args):
                           'fwd_traffic': (traffic or {}).get('gram_fwd'),
                           'bwd_traffic': (traffic or {}).get('gram_bwd')},
         'loss_first_last': [first_loss, last_loss],
-        'nonfinite_clips': bad,
+        'nonfinite_clips': bad[0],
+        'range_flagged_clips': bad[1],
     }
     if dev.type == 'cuda':
         out.update(grad_check(Eng, args.precision, dev, args.gatys))

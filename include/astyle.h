@@ -97,7 +97,11 @@ int ast_set_targets(ast_ctx* ctx, const float* phi_c_dev, int phi_c_shared,
  * whatever gamma is, and enters the gradient only through gamma. */
 int ast_loss_grad(ast_ctx* ctx, const float* x_dev, float* grad_dev, float* parts_dev, void* stream);
 
-/* Per-clip flags of the last ast_loss_grad into flags_dev [batch] (int, device), OR of:
+/* Per-clip flags accumulated (OR) over every ast_loss_grad since the last reset, into flags_dev
+ * [batch] (int, device) -- sticky, so an out-of-range line-search trial inside a device
+ * L-BFGS-B epoch stays visible after the epoch (the reference's ScipyOptimizerInterface sees
+ * every evaluation, methods.py:164-181).  Reset: ast_range_flags_reset, ast_lbfgs_begin with
+ * x0 or a continuation, and ast_create.  Bits:
  *   AST_RANGE_NONFINITE  the clip's loss parts or gradient hold a NaN / Inf (the reference
  *                        would hand them to the next L-BFGS-B step);
  *   AST_RANGE_ACT        precision 2: a per-clip max |e_l| or the forward intermediate bound
@@ -113,6 +117,8 @@ int ast_loss_grad(ast_ctx* ctx, const float* x_dev, float* grad_dev, float* part
 #define AST_RANGE_GRAD 4
 #define AST_RANGE_TINY 8
 int ast_range_flags(ast_ctx* ctx, int* flags_dev, void* stream);
+/* Clear the accumulated range flags (stream-ordered; graph-capturable). */
+int ast_range_flags_reset(ast_ctx* ctx, void* stream);
 
 /* Change gamma (methods.py:125) without rebuilding the context. */
 int ast_set_gamma(ast_ctx* ctx, float gamma);

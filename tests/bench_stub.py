@@ -1,6 +1,6 @@
 """CPU stand-in for StyleEngine, for the CPU tests of bench.py's launcher and rank logic
 (tests/test_distributed.py).  It implements the engine surface bench.py and AdamLoop call
-(embeds / set_targets / loss_grad / adam_step_dev / timing) with a small deterministic
+(embeds / set_targets / loss_grad / adam_step_dev / range flags / timing) with a small deterministic
 per-clip problem, so a clip's result depends only on its own inputs: the multi-rank result can
 be compared clip by clip with a single-process one."""
 from __future__ import annotations
@@ -49,6 +49,15 @@ class StubEngine:
         m.mul_(beta1).add_((1 - beta1) * grad)
         v.mul_(beta2).add_((1 - beta2) * grad * grad)
         x.sub_(lr * (m / (1 - beta1 ** k)) / ((v / (1 - beta2 ** k)).sqrt() + eps))
+
+    def reset_range_flags(self):
+        self._flags = torch.zeros(self.batch, dtype=torch.int32)
+
+    def range_flags(self, reset=False):
+        f = getattr(self, '_flags', torch.zeros(self.batch, dtype=torch.int32)).clone()
+        if reset:
+            self.reset_range_flags()
+        return f
 
     def timing(self, enable):
         if enable:

@@ -187,3 +187,34 @@ def test_gamma_change_after_capture_is_not_ignored(weights, dev):
     assert float(outs[0][1][:, 3].abs().sum()) > 0        # the regulariser term is live
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_range_flags_cover_every_evaluation_of_a_device_epoch(weights, dev):
+    """the split range guard must see every evaluation of a device L-BFGS-B epoch,
+    not only the last.  Mid-epoch, one out-of-range trial of clip 0 (x = 1e30, as a runaway
+    line-search step would evaluate) is run through the same context; the epoch then continues
+    and ends at an in-range point.  After the epoch clip 0 is flagged, its neighbour is not, and
+    the end point alone is unflagged (what the round-3 last-evaluation flags reported)."""
+    from audio_style_transfer_amd.engine import LbfgsLoop
+    B, T = 2, 2048
+    eng, _, x0 = _setup(B, T, weights, dev, precision='split')
+    loop = LbfgsLoop(eng, maxiter=6)
+    loop.begin(torch.tensor(x0))
+    assert eng.range_flags().cpu().tolist() == [0, 0]       # begin resets
+    for i in range(40):
+        loop.step()
+        if i == 4:
+            trial = loop.x.clone()
+            trial[0] = 1e30
+            eng.loss_grad(trial)
+        if i > 4 and not loop.state()[0][:, 0].any():
+            break
+    info, x64 = loop.state(with_x=True)
+    assert not info[:, 0].any(), info
+    f = eng.range_flags().cpu().tolist()
+    assert f[0] & (1 | 2) and f[1] == 0, f
+    eng.reset_range_flags()
+    eng.loss_grad(x64.float().contiguous())
+    assert eng.range_flags().cpu().tolist() == [0, 0]
+    loop.begin(None)                                          # the next epoch starts clean
+    assert eng.range_flags().cpu().tolist() == [0, 0]

@@ -1,6 +1,8 @@
 """The alternative split forward block kernels against the default one-wave kernel: the
-role-split kernel (block_fwd_roles.hip, ASTYLE_FWD_ROLES=1) and the double-buffered-image kernel
-(block_fwd_db.hip, ASTYLE_FWD_DB=1).  Same split numerics, so every extract must be bit-identical, on every
+role-split kernel (tools/variants/block_fwd_roles.hip, ASTYLE_FWD_ROLES=1) and the double-buffered-
+image kernel (tools/variants/block_fwd_db.hip, ASTYLE_FWD_DB=1).  They are not part of the shipped
+libastyle.so: the tools-only build ``ASTYLE_VARIANT=fwdvariants python audio_style_transfer_amd/
+_build.py`` makes libastyle_fwdvariants.so, and these tests skip without it.  Same split numerics, so every extract must be bit-identical, on every
 dilation layout (T = 3584: one segment with halo rows, per-column tap masks where 64-position tiles
 start and end inside sub-sequences; T = 2048: the 32-position two-segment layout) and with several
 clips per launch.  The knob is read once per process, so each run is a child process
@@ -18,6 +20,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VLIB = os.path.join(ROOT, 'audio_style_transfer_amd', 'libastyle_fwdvariants.so')
 IDS = [0, 1, 5, 6, 8, 9, 10, 19, 25, 29, 30]
 
 CHILD = r'''
@@ -38,7 +41,7 @@ np.savez(out, **{'e%d' % i: eng.extract(i).cpu().numpy() for i in ids})
 
 
 def _run(B, T, knob, path):
-    env = dict(os.environ, ASTYLE_FWD_ROLES='0', ASTYLE_FWD_DB='0')
+    env = dict(os.environ, ASTYLE_FWD_ROLES='0', ASTYLE_FWD_DB='0', ASTYLE_LIB=VLIB)
     if knob:
         env[knob] = '1'
     subprocess.run([sys.executable, '-c', CHILD, ROOT, str(B), str(T), path, json.dumps(IDS)],
@@ -51,6 +54,8 @@ def _run(B, T, knob, path):
 @pytest.mark.parametrize('B,T', [(3, 3584), (2, 2048), (2, 512)])
 def test_alt_forward_bit_identical(B, T, knob):
     assert torch.cuda.is_available(), 'gpu tests need an MI355X'
+    if not os.path.exists(VLIB):
+        pytest.skip('tools-only variant build libastyle_fwdvariants.so not built')
     with tempfile.TemporaryDirectory() as d:
         ref = _run(B, T, None, os.path.join(d, 'one.npz'))
         got = _run(B, T, knob, os.path.join(d, 'alt.npz'))
