@@ -95,6 +95,7 @@ int set_error(int code, const std::string& msg) { return fail(code, msg); }   //
 struct ast_ctx {
     ast_cfg cfg;
     int dev = 0;
+    int cus = 0;                            // persistent block kernels' workgroup budget (0 = every CU)
     int nblk = 0;
     bool need_bott = false;
     int nu = 0, uid[32];
@@ -321,6 +322,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
             a.dn_log2 = (l + 1) % 10; a.nn = c.T >> a.dn_log2;
             a.kd = x->kd[l]; a.kr = x->kr[l];
             a.wdn = x->wdn[l]; a.bdm = x->bdm[l];
+            a.cus = x->cus;
             launch_block_fwd_s(a, s);
         } else if (x->bf) {
             FwdArgsC a;
@@ -927,6 +929,7 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
             a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
             a.kd = x->kd[l]; a.kr = x->kr[l];
             a.wrn = x->wrn[l];
+            a.cus = x->cus;
             launch_block_bwd_s(a, s);
         } else if (x->bf) {
             // the bf16 chain holds d loss / d e_l with D_l already added (the kernel adds it)
@@ -985,6 +988,13 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
 int ast_range_flags(ast_ctx* x, int* flags, void* stream) {
     if (!x || !flags) return fail(AST_E_ARG, "null argument");
     HIPCHK(hipMemcpyAsync(flags, x->rflags, (size_t)x->cfg.batch * 4, hipMemcpyDeviceToDevice, S(stream)));
+    return 0;
+}
+
+int ast_set_cu_limit(ast_ctx* x, int cus) {
+    if (!x) return fail(AST_E_ARG, "null argument");
+    if (cus < 0) return fail(AST_E_ARG, "cu limit must be >= 0 (0 = every CU)");
+    x->cus = cus;
     return 0;
 }
 

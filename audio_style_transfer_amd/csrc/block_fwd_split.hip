@@ -457,7 +457,7 @@ void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
     a.fn = make_fdiv((uint32_t)a.n);
     a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));
     const int nt = a.B * (a.T / TMS);
-    const dim3 grid(std::min(nt, sw::num_cus()));
+    const dim3 grid(std::min(nt, a.cus > 0 ? std::min(a.cus, sw::num_cus()) : sw::num_cus()));
     Layout ly;
     const bool masked = pick_layout(a.n, ly);
     if (masked) hipLaunchKernelGGL((k_block_fwd_s<true, false>), grid, dim3(FT), 0, s, a, ly);

@@ -195,6 +195,7 @@ struct FwdArgsS {
     int dn_log2, nn;       // next layer: log2 dilation, T / dilation
     int kd, kr;            // weight exponents
     float wdn, bdm;        // max_co sum_{tap,ci} |W_d|, max |b_d|: |u| <= wdn max|e_l| + bdm
+    int cus;               // workgroups (CUs) the persistent grid may use; 0 = every CU
     FDiv fn, ft;           // by n; by B (or T / 64: splitwave.h tile order): set by the launcher
 };
 
@@ -211,6 +212,7 @@ struct BwdArgsS {
     int B, T, d, n;
     int kd, kr;
     float wrn;             // max_ci sum_co |W_r|: |W_r tot| <= wrn max|tot|
+    int cus;               // workgroups (CUs) the persistent grid may use; 0 = every CU
     FDiv fn, ft;           // by n; by B (or T / 64: splitwave.h tile order): set by the launcher
 };
 

@@ -158,6 +158,12 @@ class StyleEngine:
         _lib.check(self.lib.ast_set_targets(self.h, self._ptr(phi_c), int(c_shared),
                                             self._ptr(phi_s), int(s_shared)))
 
+    def set_cu_limit(self, cus: int) -> None:
+        """At most ``cus`` CUs for the persistent split block kernels (0 = all): for running
+        several engines (disjoint clip groups) concurrently on one GPU, one stream each."""
+        _lib.check(self.lib.ast_set_cu_limit(self.h, int(cus)))
+        self.gen += 1   # captured graphs hold the grid size: recapture
+
     def set_gamma(self, gamma: float) -> None:
         """The STFT regulariser weight (--gamma, methods.py:125)."""
         _lib.check(self.lib.ast_set_gamma(self.h, float(gamma)))

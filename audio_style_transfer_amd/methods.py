@@ -59,7 +59,7 @@ class GatysNet(object):
                  logdir='./log', figdir='./data/fig', stack=0, batch_size=16384, sr=16000,
                  cont_lyr_ids=[29], nb_channels=128, cnt_channels=128, gatys=False,
                  style_lyr_ids=None, precision='split', device=None, weights=None, plots=True,
-                 optimizer='scipy'):
+                 optimizer='scipy', engine_cls=StyleEngine):
         self.logdir = logdir
         self.savepath = savepath
         self.checkpoint_path = checkpoint_path
@@ -74,6 +74,7 @@ class GatysNet(object):
         self.device = device or torch.device('cuda', torch.cuda.current_device())
         self.plots = plots
         self.optimizer = optimizer
+        self.engine_cls = engine_cls
         if weights is None:
             weights = load_weights(checkpoint_path)
             if weights is None:
@@ -86,10 +87,10 @@ class GatysNet(object):
 
     def build(self, length, batch=1, lambd=100.0, precision=None):
         """methods.py:44-77: encoder + taps + Gram + l2norm, here one libastyle context."""
-        return StyleEngine(batch, length, self.cont_lyr_ids, self.style_lyr_ids,
-                           cnt_channels=self.cnt_channels, nb_channels=self.nb_channels,
-                           gatys=self.gatys, lambd=lambd, precision=precision or self.precision,
-                           device=self.device, weights=self.weights)
+        return self.engine_cls(batch, length, self.cont_lyr_ids, self.style_lyr_ids,
+                               cnt_channels=self.cnt_channels, nb_channels=self.nb_channels,
+                               gatys=self.gatys, lambd=lambd, precision=precision or self.precision,
+                               device=self.device, weights=self.weights)
 
     def get_embeds(self, *args, is_content=True):
         """methods.py:86-95: mu-law encode the clip and fetch embeds_c or embeds_s.  Accepts the
@@ -275,22 +276,30 @@ class GatysNet(object):
                        self.precision, optimizer)).encode())
         return h.hexdigest()
 
-    def run(self, cont_file, source, target, epochs, lambd=0.1, gamma=0.1, audio_channel=0,
-            start=1.0, resume=False):
-        """methods.py:183-216."""
+    def targets(self, cont_file, source, target, audio_channel=0, start=1.0, savepath=None):
+        """methods.py:185-213: the content clip's phi_c and the analogy style target
+        phi = l2norm(phi(content clip) + phi(target file) - phi(source file)); writes ori.wav and
+        style.wav to ``savepath`` (default self.savepath)."""
+        savepath = savepath or self.savepath
         phi_t = self.get_style_phi(target)
         phi_s = self.get_style_phi(source, show_mat=False)
         aud, _ = utils.load_audio(cont_file, sr=self.sr, audio_channel=audio_channel)
         st = int(start * self.sr - self.late)
         aud = aud[st:st + self.batch_size]
-        utils.write_wav(os.path.join(self.savepath, 'ori.wav'), aud[self.late:-self.late], self.sr)
+        utils.write_wav(os.path.join(savepath, 'ori.wav'), aud[self.late:-self.late], self.sr)
         style_aud, _ = utils.load_audio(target, sr=self.sr, audio_channel=audio_channel)
         style_aud = style_aud[st:st + self.batch_size]
-        utils.write_wav(os.path.join(self.savepath, 'style.wav'), style_aud[self.late:-self.late], self.sr)
+        utils.write_wav(os.path.join(savepath, 'style.wav'), style_aud[self.late:-self.late], self.sr)
         phi_c = self.get_embeds(aud)
         phi = self.get_embeds(aud, is_content=False)
         phi = phi + phi_t - phi_s
         phi = phi / np.sqrt(np.maximum(np.sum(phi * phi, axis=(1, 2), keepdims=True), 1e-12))
+        return phi_c, phi
+
+    def run(self, cont_file, source, target, epochs, lambd=0.1, gamma=0.1, audio_channel=0,
+            start=1.0, resume=False):
+        """methods.py:183-216."""
+        phi_c, phi = self.targets(cont_file, source, target, audio_channel, start)
         x = self.l_bfgs(phi_c, phi, epochs=epochs, lambd=lambd, gamma=gamma,
                         optimizer=self.optimizer, resume=resume)
         return utils.inv_mu_law_numpy(x[None])[0]
@@ -324,11 +333,13 @@ def piece_work(args):
                     gamma=args.gamma, start=args.start, resume=args.resume)
 
 
-def make_parser():
-    """methods.py:244-267, plus --precision / --weights / --no_plots / --optimizer / --resume."""
-    parser = argparse.ArgumentParser()
-    parser.add_argument('cont_fn', help='relative content file name')
-    parser.add_argument('style_fn', help='relative style file name')
+def make_parser(positionals=True, **kw):
+    """methods.py:244-267, plus --precision / --weights / --no_plots / --optimizer / --resume
+    (positionals=False: without cont_fn / style_fn, for the batch mode's parser)."""
+    parser = argparse.ArgumentParser(**kw)
+    if positionals:
+        parser.add_argument('cont_fn', help='relative content file name')
+        parser.add_argument('style_fn', help='relative style file name')
     parser.add_argument('--epochs', help='number of epochs, each epoch contains 100 iterations of optimization',
                         nargs='?', type=int, default=100)
     parser.add_argument('--batch_size', help='length of output signal, must be divided by 4096', nargs='?', type=int, default=16384)

@@ -9,6 +9,11 @@ barrier and the max-over-ranks of the timed region.
 """
 from __future__ import annotations
 
+import os
+import socket
+import subprocess
+import sys
+
 import numpy as np
 
 CONTENT_SEED0 = 1000     # content clips default_rng(1000 + b)
@@ -51,3 +56,33 @@ def max_over_ranks(v: float, world: int, device=None) -> float:
     t = torch.tensor([v], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(gpus: int, target, argv, env_extra=None):
+    """One process per GPU (bench.py --gpus N, the batch CLI --gpus N): when this process is
+    not already a rank of a launcher (WORLD_SIZE unset) and gpus > 1, start `gpus` ranks of
+    ``target`` (argv prefix: a script path, or ['-m', module]) under torch.distributed.run as a
+    child process -- before anything touches the GPU -- and return its exit code.  Returns
+    None when this process should run as the rank itself, 2 when WORLD_SIZE disagrees."""
+    ws_env = os.environ.get('WORLD_SIZE')
+    if ws_env is not None:
+        if int(ws_env) != gpus:
+            print('WORLD_SIZE=%s but --gpus %d' % (ws_env, gpus), file=sys.stderr)
+            return 2
+        return None
+    if gpus <= 1:
+        return None
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(gpus), '--master-addr', '127.0.0.1',
+           '--master-port', str(_free_port()), *target, *argv]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '0'))
+    env.update(env_extra or {})
+    return subprocess.call(cmd, env=env)

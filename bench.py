@@ -26,8 +26,6 @@ import argparse
 import importlib
 import json
 import os
-import socket
-import subprocess
 import sys
 import time
 
@@ -76,31 +74,11 @@ def parse(argv=None):
 
 
 # ----------------------------------------------------------------------------- launcher
-def _free_port():
-    s = socket.socket()
-    s.bind(('127.0.0.1', 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def launch(argv):
     """--gpus N without a launcher: start N ranks under torch.distributed.run as a child
-    process (nothing here has touched the GPU) and return its exit code."""
-    args = parse(argv)
-    ws_env = os.environ.get('WORLD_SIZE')
-    if ws_env is not None:
-        if int(ws_env) != args.gpus:
-            print('bench.py: WORLD_SIZE=%s but --gpus %d' % (ws_env, args.gpus), file=sys.stderr)
-            return 2
-        return None
-    if args.gpus <= 1:
-        return None
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
-           '--nproc-per-node', str(args.gpus), '--master-addr', '127.0.0.1',
-           '--master-port', str(_free_port()), os.path.abspath(__file__), *argv]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '0'))
-    return subprocess.call(cmd, env=env)
+    process (nothing here has touched the GPU) and return its exit code (shard.launch_ranks)."""
+    from audio_style_transfer_amd.shard import launch_ranks
+    return launch_ranks(parse(argv).gpus, [os.path.abspath(__file__)], argv)
 
 
 # ----------------------------------------------------------------------------- ranks

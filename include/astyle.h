@@ -120,6 +120,13 @@ int ast_range_flags(ast_ctx* ctx, int* flags_dev, void* stream);
 /* Clear the accumulated range flags (stream-ordered; graph-capturable). */
 int ast_range_flags_reset(ast_ctx* ctx, void* stream);
 
+/* Workgroup budget of the persistent split block kernels (one workgroup per CU): at most cus
+ * CUs (0 = every CU, the default).  Several contexts holding disjoint clip groups can then run
+ * concurrently on one GPU, each on its own stream: while one group's HBM-bound Gram kernels run,
+ * another's MFMA-bound block kernels use the other CUs (bench.py --groups).  A captured graph
+ * bakes the grid in: recapture after a change.  No reference counterpart (a scheduling knob). */
+int ast_set_cu_limit(ast_ctx* ctx, int cus);
+
 /* Change gamma (methods.py:125) without rebuilding the context. */
 int ast_set_gamma(ast_ctx* ctx, float gamma);
 

@@ -1,10 +1,13 @@
-"""CPU stand-in for StyleEngine, for the CPU tests of bench.py's launcher and rank logic
-(tests/test_distributed.py).  It implements the engine surface bench.py and AdamLoop call
-(embeds / set_targets / loss_grad / adam_step_dev / range flags / timing) with a small deterministic
-per-clip problem, so a clip's result depends only on its own inputs: the multi-rank result can
-be compared clip by clip with a single-process one."""
+"""CPU stand-ins for StyleEngine and LbfgsLoop, for the CPU tests of bench.py's and the batch
+CLI's launcher and rank logic (tests/test_distributed.py, tests/test_batch.py).  StubEngine
+implements the engine surface bench.py, AdamLoop, GatysNet and the batch mode call (embeds /
+set_targets / set_gamma / loss_grad / adam_step_dev / range flags / timing) with a small
+deterministic per-clip problem, so a clip's result depends only on its own inputs: the
+multi-rank result can be compared clip by clip with a single-process one.  LbfgsLoop drives
+scipy's L-BFGS-B per active clip through the same interface as engine.LbfgsLoop."""
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 
@@ -15,6 +18,9 @@ class StubEngine:
             raise RuntimeError('StubEngine is the CPU stand-in (device cpu)')
         self.batch, self.T, self.device = int(batch), int(T), torch.device(device)
         self.lambd = float(lambd)
+        self.precision = precision
+        self.gamma = 0.0
+        self.style_shape = (1, 4, 4)
         self._t = None
         self.calls = 0
 
@@ -26,7 +32,13 @@ class StubEngine:
         return emb_c, emb_s.reshape(B, 1, 4, 4) if style else None
 
     def set_targets(self, phi_c, phi_s):
+        phi_c = torch.as_tensor(phi_c, dtype=torch.float32)
+        if phi_c.dim() == 2:
+            phi_c = phi_c[None].expand(self.batch, -1, -1)
         self._t = (phi_c[..., 0] * 128.0, phi_s)
+
+    def set_gamma(self, gamma):
+        self.gamma = float(gamma)
 
     def loss_grad(self, x, grad=None, parts=None):
         d = x - self._t[0]
@@ -70,3 +82,40 @@ class StubEngine:
 
     def close(self):
         pass
+
+
+class LbfgsLoop:
+    """engine.LbfgsLoop's interface (minimize / state / parts) over StubEngine: scipy L-BFGS-B
+    (maxiter, default options) per active clip, the other clips' points held fixed."""
+
+    def __init__(self, eng, m=10, maxiter=100, **kw):
+        self.eng, self.maxiter = eng, int(maxiter)
+        self.x64 = torch.zeros(eng.batch, eng.T, dtype=torch.float64)
+        self.parts = torch.zeros(eng.batch, 4)
+        self.info = np.zeros((eng.batch, 4), np.int32)
+
+    def minimize(self, x0=None, active=None, **kw):
+        from scipy.optimize import minimize
+        eng = self.eng
+        if x0 is not None:
+            self.x64 = torch.as_tensor(x0, dtype=torch.float64).clone()
+        act = np.ones(eng.batch, bool) if active is None else np.asarray(active).astype(bool)
+        self.info[:] = 0
+        for b in np.flatnonzero(act):
+            base = self.x64.float()
+
+            def fg(v, b=b):
+                x = base.clone()
+                x[b] = torch.from_numpy(v.astype(np.float32))
+                parts, grad = eng.loss_grad(x)
+                self.parts[b] = parts[b]
+                return float(parts[b, 0]), grad[b].double().numpy()
+
+            res = minimize(fg, self.x64[b].float().double().numpy(), jac=True, method='L-BFGS-B',
+                           options={'maxiter': self.maxiter})
+            self.x64[b] = torch.from_numpy(res.x)
+            self.info[b] = (0, res.nit, res.nfev, 1)
+        return self.info.copy()
+
+    def state(self, with_x=False):
+        return self.info.copy(), (self.x64.clone() if with_x else None)

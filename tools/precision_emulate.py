@@ -10,7 +10,7 @@ round them, and the result is rounded to fp32 (the MFMA accumulates in fp32).  S
 The gradient rel-L2 against the fp64 oracle is printed for each combination of
 (encoder scheme, Gram forward scheme, Gram backward scheme).
 
-  python tools/precision_emulate.py [T] [tag]
+  python tools/precision_emulate.py [T] [tag] [wino]   (wino: Winograd F(2,3) dilated convs)
 """
 import os
 import sys
@@ -94,7 +94,38 @@ def conv_t(g, W, d):
     return F.conv_transpose1d(g[None], W, None, padding=((k - 1) // 2) * d, dilation=d)[0]
 
 
-def run(x, Wd, phi_c, phi_s, kw, enc='fp32', gf='fp32', gb='fp32', store='fp32'):
+def wino(x, W, d, scheme):
+    """The dilated conv (x [C, T], W OIK, K = 3, SAME) as Winograd F(2,3) over output pairs
+    (positions 2j, 2j+1 of each sub-sequence t = s + k d, masked.py:57-86): the transformed
+    inputs d0 = x_{2j-1} - x_{2j+1}, d1 = x_{2j} + x_{2j+1}, d2 = x_{2j+1} - x_{2j},
+    d3 = x_{2j} - x_{2j+2} formed in fp32 (as the kernel's conversion would), the transformed
+    weights G = (W0, (W0+W1+W2)/2, (W0-W1+W2)/2, W2) in fp64 then split, four products m_i =
+    G_i d_i under `scheme`, y_{2j} = m0 + m1 + m2, y_{2j+1} = m1 - m2 - m3 in fp32."""
+    C, T = x.shape
+    n = T // d
+    assert n % 2 == 0
+    X = x.reshape(C, n, d)                                    # X[:, k, s] = x[:, k d + s]
+    Z = torch.zeros(C, 1, d, dtype=x.dtype)
+    Xp = torch.cat([Z, X, Z, Z], 1)                           # k = -1 .. n + 1
+    xm1, x0, x1, x2 = (Xp[:, 2 * np.arange(n // 2) + o] for o in (0, 1, 2, 3))
+    ds = [r32(xm1 - x1), r32(x0 + x1), r32(x1 - x0), r32(x0 - x2)]
+    W0, W1, W2 = W[:, :, 0], W[:, :, 1], W[:, :, 2]
+    Gs = [W0, (W0 + W1 + W2) / 2, (W0 - W1 + W2) / 2, W2]
+    mm = lambda a, b: torch.einsum('oc,cjs->ojs', b, a)
+    m = [prod(scheme, mm, dd, G) for dd, G in zip(ds, Gs)]
+    y0 = r32(r32(m[0] + m[1]) + m[2])
+    y1 = r32(r32(m[1] - m[2]) - m[3])
+    Y = torch.stack([y0, y1], 2).reshape(W.shape[0], n, d)   # k = 2j, 2j + 1
+    return Y.reshape(W.shape[0], T)
+
+
+def wino_t(g, W, d, scheme):
+    """conv_transpose1d of the dilated conv = the conv with taps (W2^T, W1^T, W0^T)."""
+    Wt = W.permute(1, 0, 2).flip(2).contiguous()
+    return wino(g, Wt, d, scheme)
+
+
+def run(x, Wd, phi_c, phi_s, kw, enc='fp32', gf='fp32', gb='fp32', store='fp32', winograd=False):
     R = r32 if store == 'fp32' else f16x2
     if enc == 'fp64':
         R = lambda a: a
@@ -108,7 +139,10 @@ def run(x, Wd, phi_c, phi_s, kw, enc='fp32', gf='fp32', gb='fp32', store='fp32')
         dd = O.dilation_of(l)
         Wdl, bdl = Wd['ae_dilatedconv_%d/W' % (l + 1)], Wd['ae_dilatedconv_%d/biases' % (l + 1)]
         Wrl, brl = Wd['ae_res_%d/W' % (l + 1)], Wd['ae_res_%d/biases' % (l + 1)]
-        u = R(prod(enc, lambda a, b: conv(a, b, dd), torch.relu(e), Wdl) + bdl[:, None])
+        if winograd and e.shape[1] // dd >= 2:
+            u = R(wino(torch.relu(e), Wdl, dd, enc) + bdl[:, None])
+        else:
+            u = R(prod(enc, lambda a, b: conv(a, b, dd), torch.relu(e), Wdl) + bdl[:, None])
         y = prod(enc, lambda a, b: conv(a, b, 1), torch.relu(u), Wrl) + brl[:, None]
         e = R(e + y)
         es.append(e)
@@ -154,7 +188,10 @@ def run(x, Wd, phi_c, phi_s, kw, enc='fp32', gf='fp32', gb='fp32', store='fp32')
         Wdl, Wrl = Wd['ae_dilatedconv_%d/W' % (l + 1)], Wd['ae_res_%d/W' % (l + 1)]
         gv = prod(enc, lambda a, b: conv_t(a, b, 1), g, Wrl)
         gu = R(gv * (us[l] > 0))
-        gh = prod(enc, lambda a, b: conv_t(a, b, dd), gu, Wdl)
+        if winograd and gu.shape[1] // dd >= 2:
+            gh = wino_t(gu, Wdl, dd, enc)
+        else:
+            gh = prod(enc, lambda a, b: conv_t(a, b, dd), gu, Wdl)
         g = R(g + gh * (es[l] > 0))
     gx = conv_t(g, W0, 1)[0] / 128.0
     return float(content), float(style), gx.numpy()
@@ -184,6 +221,15 @@ def main():
     _, _, ref = run(x, Wd, phi_c, phi_s, kw, enc='fp64', gf='fp64', gb='fp64')
     _, ogr = O.loss_and_grad(x, W, phi_c=phi_c, phi_s=phi_s, **full)
     print('restatement vs oracle fp64: %.3g' % (np.linalg.norm(ref - ogr) / np.linalg.norm(ogr)))
+    if 'wino' in sys.argv:   # Winograd F(2,3) dilated convs (fwd + bwd) vs the direct form
+        _, _, w64 = run(x, Wd, phi_c, phi_s, kw, enc='fp64', gf='fp64', gb='fp64', winograd=True)
+        print('winograd fp64 vs direct fp64: %.3g' % (np.linalg.norm(w64 - ref) / np.linalg.norm(ref)))
+        for enc, gf, gb, wg in [('fp32', 'fp32', 'fp32', False), ('fp32', 'fp32', 'fp32', True),
+                                ('f16x3', 'split3', 'split3', False), ('f16x3', 'split3', 'split3', True)]:
+            c, s_, g = run(x, Wd, phi_c, phi_s, kw, enc=enc, gf=gf, gb=gb, winograd=wg)
+            print('enc %-6s%s gram %-6s grad rel-L2 %.3g' % (enc, ' winograd' if wg else ' direct  ', gf,
+                  np.linalg.norm(g - ref) / np.linalg.norm(ref)), flush=True)
+        return
     for enc, gf, gb, st in [('fp32', 'fp32', 'fp32', 'fp32'), ('split3', 'fp32', 'fp32', 'fp32'),
                             ('f16x3', 'fp32', 'fp32', 'fp32'), ('f16x3', 'fp32', 'fp32', 'f16x2'),
                             ('f16x3', 'bf16', 'fp32', 'fp32'), ('f16x3', 'bf16', 'bf16', 'fp32'),
