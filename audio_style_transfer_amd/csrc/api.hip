@@ -297,7 +297,8 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
     const ast_cfg& c = x->cfg;
     if (x->split) {
         HIPCHK(hipMemsetAsync(x->gmax_e, 0, (size_t)(NBLK_MAX + 1) * c.batch * 4, s));
-        launch_startconv_fwd((const float*)xd, (float*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s,
+        // e_0 is not stored: block 0 recomputes it from x (FwdArgsS::xin); masks and max only
+        launch_startconv_fwd((const float*)xd, (float*)nullptr, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s,
                              (uint16_t*)x->me, x->gmax_e);
     } else if (x->bf) launch_startconv_fwd((const float*)xd, (u16*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s, (uint16_t*)x->me);
     else launch_startconv_fwd((const float*)xd, (float*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s);
@@ -323,6 +324,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
             a.kd = x->kd[l]; a.kr = x->kr[l];
             a.wdn = x->wdn[l]; a.bdm = x->bdm[l];
             a.cus = x->cus;
+            a.xin = l == 0 ? xd : nullptr; a.w0 = x->wts + W0_OFF; a.b0 = x->wts + B0_OFF;
             launch_block_fwd_s(a, s);
         } else if (x->bf) {
             FwdArgsC a;
@@ -930,6 +932,9 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
             a.kd = x->kd[l]; a.kr = x->kr[l];
             a.wrn = x->wrn[l];
             a.cus = x->cus;
+            // block 0: the start conv's backward folded in; chain[0] holds the wave partials
+            a.w0 = x->wts + W0_OFF;
+            a.spart = l == 0 ? (float*)x->chain[0] : nullptr;
             launch_block_bwd_s(a, s);
         } else if (x->bf) {
             // the bf16 chain holds d loss / d e_l with D_l already added (the kernel adds it)
@@ -955,7 +960,8 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
         }
     }
     tmark(x, s);
-    if (x->bf) launch_startconv_bwd((const u16*)x->chain[0], grad, x->wts + W0_OFF, c.batch, c.T, s);
+    if (x->split) launch_startx_gx((const float*)x->chain[0], grad, c.batch, c.T, s);
+    else if (x->bf) launch_startconv_bwd((const u16*)x->chain[0], grad, x->wts + W0_OFF, c.batch, c.T, s);
     else launch_startconv_bwd((const float*)x->chain[0], grad, x->wts + W0_OFF, c.batch, c.T, s);
     const int nb = std::min(c.nb_channels, C);
     if (c.gatys)

@@ -29,6 +29,8 @@
 // The first tile is peeled so every loop iteration issues the same vector-memory sequence.
 #include "splitwave.h"
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 namespace ast {
@@ -40,11 +42,16 @@ constexpr int ISLOT = IROWS * RS;
 constexpr int GROWS = 68;             // g_u image rows (66 / 68 used; 66 takes unused halo writes)
 constexpr int LA = 2;                 // B-fragment lookahead (steps)
 
-template <bool MASKED, bool ONESEG, bool HAS_D>
+// SX (block 0, one-segment layout, d = 1, no D_0): the start conv's backward folded into the
+// epilogue -- out = d loss / d e_0 is not stored; per position the wave's three dot products
+// sum_c W0[k][c] out[t][c] over its 32 channels go to spart (launch_startx_gx sums the four
+// waves and forms d loss / d x): no 2 GiB g_0 round trip (model.py:82-93)
+template <bool MASKED, bool ONESEG, bool HAS_D, bool SX>
 __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     __shared__ __attribute__((aligned(16))) uint8_t XS[ISLOT];        // split tot image
     __shared__ __attribute__((aligned(16))) uint8_t XG[GROWS * RS];   // split g_u image
     __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];     // fp32 tot + D_l rows
+    __shared__ __attribute__((aligned(16))) float W0S[SX ? 3 * C : 4];   // SX: W0 [3][C]
 
     const int tiles = a.T / TMS;
     const int ntiles = a.B * tiles;
@@ -74,6 +81,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     pin_all(wd, wr);
     // the g_u image's pad / unused halo rows stay zero (only column and halo rows are written)
     for (int i = tid; i < GROWS * RS / 16; i += FT) reinterpret_cast<uint4*>(XG)[i] = make_uint4(0, 0, 0, 0);
+    if (SX)   // (read after the first tile's T barrier)
+        for (int i = tid; i < 3 * C; i += FT) W0S[i] = a.w0[i];
 
     int Lc[2], toff[2];
 #pragma unroll
@@ -244,8 +253,11 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     const uint32_t colo[2] = {(uint32_t)((toff[0] * C + chb) * 4), (uint32_t)((toff[1] * C + chb) * 4)};
     uint32_t ocol = 0;
     float4 oe, oo;
+    float sk0 = 0.f, sk1 = 0.f, sk2 = 0.f;   // SX: the lane's dot products over its 16 channels
+    size_t sxo = 0;                          // SX: spart float index of (column, wave)
     auto epi_begin = [&](const Tile& et, int J) {
-        if (MASKED) dst = a.gout + ((size_t)et.b * a.T + ctime(et, 32 * J + r, toff[J])) * C + chb;
+        if (SX) sxo = (((size_t)et.b * a.T + ctime(et, 32 * J + r, toff[J])) * 4 + w) * 4;
+        else if (MASKED) dst = a.gout + ((size_t)et.b * a.T + ctime(et, 32 * J + r, toff[J])) * C + chb;
         else { rs_o = mk_rsrc(a.gout + ((size_t)et.b * a.T + et.tb) * C); ocol = colo[J]; }
     };
     auto epi_part = [&](int J, int g, int part, const uint8_t* er, uint32_t mw, float inv2) {
@@ -256,10 +268,23 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             oo.y = fmaf(keep_if(acc2[J][4 * g + 1], mw, 4 + g), inv2, oe.y);
             oo.z = fmaf(keep_if(acc2[J][4 * g + 2], mw, 8 + g), inv2, oe.z);
             oo.w = fmaf(keep_if(acc2[J][4 * g + 3], mw, 12 + g), inv2, oe.w);
-            if (MASKED) *reinterpret_cast<float4*>(dst + 8 * g) = oo;
+            if (SX) {
+                const float4 q0 = *reinterpret_cast<const float4*>(&W0S[chb + 8 * g]);
+                const float4 q1 = *reinterpret_cast<const float4*>(&W0S[C + chb + 8 * g]);
+                const float4 q2 = *reinterpret_cast<const float4*>(&W0S[2 * C + chb + 8 * g]);
+                sk0 = fmaf(q0.w, oo.w, fmaf(q0.z, oo.z, fmaf(q0.y, oo.y, fmaf(q0.x, oo.x, sk0))));
+                sk1 = fmaf(q1.w, oo.w, fmaf(q1.z, oo.z, fmaf(q1.y, oo.y, fmaf(q1.x, oo.x, sk1))));
+                sk2 = fmaf(q2.w, oo.w, fmaf(q2.z, oo.z, fmaf(q2.y, oo.y, fmaf(q2.x, oo.x, sk2))));
+            } else if (MASKED) *reinterpret_cast<float4*>(dst + 8 * g) = oo;
             else bst4(rs_o, ocol + 32 * g, 0u, oo);
         } else {
             omax = fmaxf(omax, fmaxf(fmaxf(fabsf(oo.x), fabsf(oo.y)), fmaxf(fabsf(oo.z), fabsf(oo.w))));
+            if (SX && g == 3) {   // the column's 16 channels done: + the other half's 16 -> spart
+                const float o0 = __shfl_xor(sk0, 32), o1 = __shfl_xor(sk1, 32), o2 = __shfl_xor(sk2, 32);
+                if (h == 0)
+                    *reinterpret_cast<float4*>(a.spart + sxo) = make_float4(sk0 + o0, sk1 + o1, sk2 + o2, 0.f);
+                sk0 = sk1 = sk2 = 0.f;
+            }
         }
     };
     auto epi_max = [&](int b) {
@@ -416,10 +441,14 @@ void launch_block_bwd_s(const BwdArgsS& a0, hipStream_t s) {
     Layout ly;
     const bool masked = pick_layout(a.n, ly);
     const bool oneseg = !masked && ly.M == TMS;
-#define BWD_LAUNCH(M, O, D) hipLaunchKernelGGL((k_block_bwd_s<M, O, D>), grid, dim3(FT), 0, s, a, ly)
-    if (masked) { if (a.dadd) BWD_LAUNCH(true, false, true); else BWD_LAUNCH(true, false, false); }
-    else if (oneseg) { if (a.dadd) BWD_LAUNCH(false, true, true); else BWD_LAUNCH(false, true, false); }
-    else { if (a.dadd) BWD_LAUNCH(false, false, true); else BWD_LAUNCH(false, false, false); }
+    if (a.spart && (!oneseg || a.dadd || a.d != 1)) { fprintf(stderr, "block_bwd_s: spart needs d = 1, no D\n"); abort(); }
+#define BWD_LAUNCH(M, O, D, X) hipLaunchKernelGGL((k_block_bwd_s<M, O, D, X>), grid, dim3(FT), 0, s, a, ly)
+    if (masked) { if (a.dadd) BWD_LAUNCH(true, false, true, false); else BWD_LAUNCH(true, false, false, false); }
+    else if (oneseg) {
+        if (a.dadd) BWD_LAUNCH(false, true, true, false);
+        else if (a.spart) BWD_LAUNCH(false, true, false, true);
+        else BWD_LAUNCH(false, true, false, false);
+    } else { if (a.dadd) BWD_LAUNCH(false, false, true, false); else BWD_LAUNCH(false, false, false, false); }
 #undef BWD_LAUNCH
 }
 

@@ -26,6 +26,7 @@
 // floor of 6.2k; moving the loads / conversions between phases does not change the tile time.
 #include "splitwave.h"
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -37,7 +38,10 @@ constexpr int IROWS = 72;             // image / residual rows: 66 or 68 used, 9
 constexpr int ISLOT = IROWS * RS;     // bytes per image / residual buffer
 constexpr int LA = 2;                 // B-fragment lookahead (steps)
 
-template <bool MASKED, bool ONESEG>
+// XIN (block 0, one-segment layout, d = 1): the rows of e_0 are recomputed from the audio
+// (e0_val: three samples per row, W0 / b0 of the lane's four channels in registers) instead of
+// loaded, so the start conv writes no e_0 tensor (model.py:82-93 folded into block 0)
+template <bool MASKED, bool ONESEG, bool XIN>
 __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     __shared__ __attribute__((aligned(16))) uint8_t IMG[ISLOT];     // split relu(e_l) image
     __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];   // fp32 e_l (residual) rows
@@ -107,8 +111,25 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     }
     const uint32_t row1 = (uint32_t)(a.d * C * 4 + 4 * cq), row64 = (uint32_t)(TMS * a.d * C * 4 + 4 * cq);   // image row 64 (time tb + 63 d)
 
-    float4 ld[NU];          // rows of the next tile to convert
+    float4 ld[NU];          // rows of the next tile to convert (XIN: x[t - 1], x[t], x[t + 1])
+    uint32_t xedge = 0;     // XIN: bit k = unit k's row at t = 0, bit 16 + k: at t = T - 1
+    float w0r[3][4], b0r[4];
+    if (XIN) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            w0r[0][i] = a.w0[cq + i]; w0r[1][i] = a.w0[C + cq + i]; w0r[2][i] = a.w0[2 * C + cq + i];
+            b0r[i] = a.b0[cq + i];
+        }
+    }
     auto load_unit = [&](const Tile& t, int k) {
+        if (XIN) {
+            // row L = time tb + L - 1 (d = 1); rows outside the clip are zeroed at conversion
+            const int tt = min(max(t.tb + 8 * k + lr - 1, 0), a.T - 1);
+            const float* xr = a.xin + (size_t)t.b * a.T;
+            ld[k] = make_float4(xr[max(tt - 1, 0)], xr[tt], xr[min(tt + 1, a.T - 1)], 0.f);
+            xedge = (xedge & ~(0x10001u << k)) | (tt == 0 ? 1u << k : 0u) | (tt == a.T - 1 ? 0x10000u << k : 0u);
+            return;
+        }
         if (MASKED) {
             const int L = 8 * k + lr;
             // row L = position p0 + L - 1, clamped into the clip (rows 0 / 65 are real
@@ -138,6 +159,13 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     // conversion of unit k: raw fp32 -> residual buffer er; relu, scale, split -> image
     auto conv_unit = [&](int k, uint8_t* er, float s, uint32_t zb) {
         float4 v = ld[k];
+        if (XIN) {   // e_0 of the lane's four channels (x[-1] = x[T] = 0)
+            const float xm = (xedge >> k) & 1u ? 0.f : v.x, x0 = v.y, xp = (xedge >> (16 + k)) & 1u ? 0.f : v.z;
+            v.x = e0_val(w0r[0][0], w0r[1][0], w0r[2][0], b0r[0], xm, x0, xp);
+            v.y = e0_val(w0r[0][1], w0r[1][1], w0r[2][1], b0r[1], xm, x0, xp);
+            v.z = e0_val(w0r[0][2], w0r[1][2], w0r[2][2], b0r[2], xm, x0, xp);
+            v.w = e0_val(w0r[0][3], w0r[1][3], w0r[2][3], b0r[3], xm, x0, xp);
+        }
         *reinterpret_cast<float4*>(er + ero + 8 * k * RS) = v;
         const float sk = (zb >> k) & 1u ? 0.f : s;
         v.x = __int_as_float(max(__float_as_int(v.x), 0)); v.y = __int_as_float(max(__float_as_int(v.y), 0));
@@ -450,8 +478,9 @@ static bool env_on(const char* k) { const char* e = getenv(k); return e && atoi(
 
 void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
 #ifdef ASTYLE_FWD_VARIANTS
-    if (env_on("ASTYLE_FWD_ROLES")) { launch_block_fwd_roles(a0, s); return; }
-    if (env_on("ASTYLE_FWD_DB")) { launch_block_fwd_db(a0, s); return; }
+    // (block 0 recomputes e_0 from x, which the variants do not: they run blocks 1..)
+    if (!a0.xin && env_on("ASTYLE_FWD_ROLES")) { launch_block_fwd_roles(a0, s); return; }
+    if (!a0.xin && env_on("ASTYLE_FWD_DB")) { launch_block_fwd_db(a0, s); return; }
 #endif
     FwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
@@ -460,9 +489,11 @@ void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
     const dim3 grid(std::min(nt, a.cus > 0 ? std::min(a.cus, sw::num_cus()) : sw::num_cus()));
     Layout ly;
     const bool masked = pick_layout(a.n, ly);
-    if (masked) hipLaunchKernelGGL((k_block_fwd_s<true, false>), grid, dim3(FT), 0, s, a, ly);
-    else if (ly.M == TMS) hipLaunchKernelGGL((k_block_fwd_s<false, true>), grid, dim3(FT), 0, s, a, ly);
-    else hipLaunchKernelGGL((k_block_fwd_s<false, false>), grid, dim3(FT), 0, s, a, ly);
+    if (a.xin && (masked || ly.M != TMS || a.d != 1)) { fprintf(stderr, "block_fwd_s: xin needs d = 1\n"); abort(); }
+    if (masked) hipLaunchKernelGGL((k_block_fwd_s<true, false, false>), grid, dim3(FT), 0, s, a, ly);
+    else if (ly.M == TMS && a.xin) hipLaunchKernelGGL((k_block_fwd_s<false, true, true>), grid, dim3(FT), 0, s, a, ly);
+    else if (ly.M == TMS) hipLaunchKernelGGL((k_block_fwd_s<false, true, false>), grid, dim3(FT), 0, s, a, ly);
+    else hipLaunchKernelGGL((k_block_fwd_s<false, false, false>), grid, dim3(FT), 0, s, a, ly);
 }
 
 int sw::num_cus() {

@@ -103,6 +103,13 @@ __device__ __forceinline__ f32x16 mfma_bf16(uint4 a, uint4 b, f32x16 c) {
                                                     __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 // generic element access for kernels templated on the storage type (float | u16 = bf16)
+// ae_startconv of one element (model.py:82-93): e_0[t][c] = b0[c] + sum_k W0[k][c] x[t + k - 1] / 128
+// with x[-1] = x[T] = 0 (SAME).  One fixed operation order, shared by k_startconv_fwd (masks and
+// max) and the split block-0 forward that recomputes e_0 from x (the two must agree bit for bit)
+__device__ __forceinline__ float e0_val(float w0, float w1, float w2, float b, float xm, float x0, float xp) {
+    return fmaf(w2, xp * 0.0078125f, fmaf(w1, x0 * 0.0078125f, w0 * (xm * 0.0078125f))) + b;
+}
+
 __device__ __forceinline__ float ldv(const float* p, size_t i) { return p[i]; }
 __device__ __forceinline__ float ldv(const u16* p, size_t i) { return bf2f(p[i]); }
 __device__ __forceinline__ void stv(float* p, size_t i, float v) { p[i] = v; }
@@ -196,6 +203,9 @@ struct FwdArgsS {
     int kd, kr;            // weight exponents
     float wdn, bdm;        // max_co sum_{tap,ci} |W_d|, max |b_d|: |u| <= wdn max|e_l| + bdm
     int cus;               // workgroups (CUs) the persistent grid may use; 0 = every CU
+    // block 0 with the start conv folded in (xin non-null): e_l = e_0 is recomputed from the
+    // audio xin [B][T] and W0 [3][C], b0 [C] (e0_val) instead of read from ein
+    const float* xin; const float* w0; const float* b0;
     FDiv fn, ft;           // by n; by B (or T / 64: splitwave.h tile order): set by the launcher
 };
 
@@ -213,6 +223,10 @@ struct BwdArgsS {
     int kd, kr;
     float wrn;             // max_ci sum_co |W_r|: |W_r tot| <= wrn max|tot|
     int cus;               // workgroups (CUs) the persistent grid may use; 0 = every CU
+    // block 0 with the start conv's backward folded in (spart non-null): instead of gout, per
+    // position and wave the three dot products sum_c W0[k][c] out[t][c] over the wave's 32
+    // channels -> spart [B][T][4 waves][4] (k = 0..2; launch_startx_gx forms d loss / d x)
+    const float* w0; float* spart;
     FDiv fn, ft;           // by n; by B (or T / 64: splitwave.h tile order): set by the launcher
 };
 
@@ -287,6 +301,7 @@ template <typename S>
 void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b0,
                           int B, int T, hipStream_t s, uint16_t* me0 = nullptr,
                           unsigned* gmax = nullptr);
+void launch_startx_gx(const float* spart, float* gx, int B, int T, hipStream_t s);
 template <typename S>
 void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T,
                           hipStream_t s);

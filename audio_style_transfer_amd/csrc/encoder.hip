@@ -254,18 +254,20 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
         const size_t rowi = lb * SFR + it * 16 + (threadIdx.x >> 4);
         const int t = (int)(rowi % T);
         const float* xr = x + (rowi - t);
-        const float xm = t > 0 ? xr[t - 1] / 128.0f : 0.f;
-        const float x0 = xr[t] / 128.0f;
-        const float xp = t < T - 1 ? xr[t + 1] / 128.0f : 0.f;
+        const float xm = t > 0 ? xr[t - 1] : 0.f;
+        const float x0 = xr[t];
+        const float xp = t < T - 1 ? xr[t + 1] : 0.f;
         float o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (wk[0][j] * xm + wk[1][j] * x0 + wk[2][j] * xp) + bk[j];
+        for (int j = 0; j < 8; ++j) o[j] = e0_val(wk[0][j], wk[1][j], wk[2][j], bk[j], xm, x0, xp);
         // element j > 0 (the stored value: fp32, or its bf16 rounding)
         bool pos[8];
         if constexpr (sizeof(S) == 4) {
-            float4* dst = reinterpret_cast<float4*>(e0 + rowi * C + m * 8);
-            dst[0] = make_float4(o[0], o[1], o[2], o[3]);
-            dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+            if (e0) {   // (null: split mode, block 0 recomputes e_0 from x; masks and max only)
+                float4* dst = reinterpret_cast<float4*>(e0 + rowi * C + m * 8);
+                dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+                dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+            }
 #pragma unroll
             for (int j = 0; j < 8; ++j) pos[j] = o[j] > 0.f;
         } else {
@@ -375,6 +377,29 @@ __global__ void __launch_bounds__(256) k_startconv_bwd(const S* __restrict__ g0,
         gx[(size_t)b * T + t0 + i] = (A[0][i + 2] + A[1][i + 1] + A[2][i]) / 128.0f;
 }
 
+// d loss / d x from the split block-0 backward's per-wave dot products (BwdArgsS::spart):
+//   a_k[t] = sum_w spart[t][w][k],  gx[t] = (a_0[t + 1] + a_1[t] + a_2[t - 1]) / 128
+// (k_startconv_bwd's sums without the 2 GiB g_0 round trip; the wave partials summed in a fixed
+// order, so a clip's result does not depend on its batch slot)
+__global__ void __launch_bounds__(256) k_startx_gx(const float* __restrict__ sp, float* __restrict__ gx,
+                                                   int B, int T) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)B * T) return;
+    const int t = (int)(i % T);
+    auto ak = [&](int tt, int k) {
+        const float4* q = reinterpret_cast<const float4*>(sp + (i - t + tt) * 16);
+        const float v[4] = {q[0].x, q[1].x, q[2].x, q[3].x};
+        const float u[4] = {q[0].y, q[1].y, q[2].y, q[3].y};
+        const float z[4] = {q[0].z, q[1].z, q[2].z, q[3].z};
+        const float* a = k == 0 ? v : k == 1 ? u : z;
+        return ((a[0] + a[1]) + a[2]) + a[3];
+    };
+    float g = ak(t, 1);
+    if (t + 1 < T) g = ak(t + 1, 0) + g;
+    if (t > 0) g = g + ak(t - 1, 2);
+    gx[i] = g * 0.0078125f;
+}
+
 // ae_bottleneck (model.py:121-127): 1x1, 128 -> 16.  Thread per (row, out channel).
 template <typename S>
 __global__ void __launch_bounds__(256) k_bottleneck_fwd(const S* __restrict__ e,
@@ -425,6 +450,10 @@ void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b
                           hipStream_t s, uint16_t* me0, unsigned* gmax) {
     hipLaunchKernelGGL(k_startconv_fwd<S>, dim3((unsigned)((size_t)B * T / SFR)), dim3(256), 0, s, x,
                        e0, w0, b0, B, T, me0, gmax);
+}
+void launch_startx_gx(const float* spart, float* gx, int B, int T, hipStream_t s) {
+    const size_t n = (size_t)B * T;
+    hipLaunchKernelGGL(k_startx_gx, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, spart, gx, B, T);
 }
 template <typename S>
 void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T, hipStream_t s) {
