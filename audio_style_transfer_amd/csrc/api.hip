@@ -446,31 +446,40 @@ int ast_restore(ast_ctx* x, const char* prefix) {
         Checkpoint ck;
         std::string err;
         if (ck.open(prefix, &err)) return fail(AST_E_NAME, err);
-        // every encoder variable with the element count its HWIO shape has (masked.py:141-145)
-        std::vector<std::pair<std::string, int64_t>> names = {
-            {"ae_startconv/W", 3 * C}, {"ae_startconv/biases", C}, {"ae_bottleneck/W", C * 16},
-            {"ae_bottleneck/biases", 16}};
+        // every encoder variable with its HWIO shape (masked.py:136-145; Saver.restore refuses a
+        // variable whose shape differs, so a transposed or reshaped tensor is refused here too)
+        typedef std::vector<int64_t> Shape;
+        std::vector<std::pair<std::string, Shape>> names = {
+            {"ae_startconv/W", {1, 3, 1, C}}, {"ae_startconv/biases", {C}},
+            {"ae_bottleneck/W", {1, 1, C, 16}}, {"ae_bottleneck/biases", {16}}};
         for (int l = 1; l <= 30; ++l) {
-            const std::pair<const char*, int64_t> ks[4] = {{"ae_dilatedconv_%d/W", 3 * C * C},
-                                                           {"ae_dilatedconv_%d/biases", C},
-                                                           {"ae_res_%d/W", C * C},
-                                                           {"ae_res_%d/biases", C}};
+            const std::pair<const char*, Shape> ks[4] = {{"ae_dilatedconv_%d/W", {1, 3, C, C}},
+                                                         {"ae_dilatedconv_%d/biases", {C}},
+                                                         {"ae_res_%d/W", {1, 1, C, C}},
+                                                         {"ae_res_%d/biases", {C}}};
             for (const auto& k : ks) {
                 char b[64];
                 snprintf(b, sizeof b, k.first, l);
                 names.emplace_back(b, k.second);
             }
         }
+        auto str = [](const Shape& v) {
+            std::string o = "[";
+            for (size_t i = 0; i < v.size(); ++i) o += (i ? "," : "") + std::to_string(v[i]);
+            return o + "]";
+        };
         std::vector<float> buf;
         for (const auto& nm : names) {
             const CkptEntry* e = ck.find(nm.first);
             if (!e) return fail(AST_E_NAME, std::string(prefix) + ": no variable " + nm.first +
                                                 " (Saver.restore needs every encoder variable)");
             // the shape from the file is checked before anything is allocated for it
-            if (e->elements() != nm.second)
-                return fail(AST_E_NAME, nm.first + ": checkpoint holds " + std::to_string(e->elements()) +
-                                            " elements, the encoder expects " + std::to_string(nm.second));
-            buf.resize((size_t)nm.second);
+            if (e->shape != nm.second)
+                return fail(AST_E_NAME, nm.first + ": checkpoint shape " + str(e->shape) +
+                                            ", the encoder expects " + str(nm.second));
+            int64_t n = 1;
+            for (int64_t d : nm.second) n *= d;
+            buf.resize((size_t)n);
             if (ck.read_f32(*e, buf.data(), &err)) return fail(AST_E_ARG, err);
             const int rc = ast_set_weight(x, nm.first.c_str(), buf.data(), buf.size());
             if (rc) return rc;
@@ -485,8 +494,11 @@ int ast_ot_admm(const double* p_mod, const double* p_ref, int nprob, int n1, int
                 double eps, double miter, double* plan, double* pal, int* iters, void* stream) {
     if (nprob < 0 || n1 < 1 || n2 < 1 || d < 1)
         return fail(AST_E_ARG, "ast_ot_admm: need nprob >= 0 and n1, n2, d >= 1");
-    if ((long long)n1 * n2 > (1ll << 26) || ot_big_lds_bytes(n1, n2) > 160 * 1024)
-        return fail(AST_E_ARG, "ast_ot_admm: n1 * n2 must be <= 2^26 and n1 + n2 <= 20000");
+    // the workspace kernel runs one workgroup per problem over 10 n1 n2 fp64 iterates: ~80 B per
+    // cell per ADMM iteration on one CU (2^16 cells: ~5 MB, ~0.1 ms per iteration, seconds per
+    // solve at the reference's iteration counts); past that the call would run for hours
+    if ((long long)n1 * n2 > (1ll << 16) || ot_big_lds_bytes(n1, n2) > 160 * 1024)
+        return fail(AST_E_ARG, "ast_ot_admm: n1 * n2 must be <= 2^16 (and n1 + n2 <= 20000)");
     if (!(eps > 0.0) || !(miter >= 0.0))
         return fail(AST_E_ARG, "ast_ot_admm: eps must be > 0 and miter >= 0");
     if (nprob == 0) return 0;
@@ -833,7 +845,7 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     for (int t = 0; t <= NBLK_MAX; ++t) first_cg[t] = true;
     bool first_bott = true;
     const int fuse_u = fused_content_occ(x);
-    if (fuse_u >= 0)   // the Gram backward writes 64 of the occurrence's partial slots per clip
+    if (fuse_u >= 0)   // the Gram backward writes nchunk x 4 of the occurrence's partial slots per clip
         HIPCHK(hipMemsetAsync(x->cpart, 0, (size_t)c.batch * x->ncpart * 4, s));
     for (size_t i = 0; i < x->occ.size(); ++i) {
         if (fuse_u >= 0) break;

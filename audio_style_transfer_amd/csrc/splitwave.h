@@ -341,7 +341,7 @@ __device__ __forceinline__ void split2(float a0, float a1, uint32_t& hi, uint32_
 }
 
 // the same for values of either sign (the backward's tot and g_u): hi = rtz, so a - hi has
-// a's sign and lo = rne(a - hi) keeps sign(lo) == sign(hi) or lo == 0
+// a's sign and lo = rtz(a - hi) keeps sign(lo) == sign(hi) or lo == 0
 __device__ __forceinline__ void split2s(float a0, float a1, uint32_t& hi, uint32_t& lo) {
     split2(a0, a1, hi, lo);
 }

@@ -47,6 +47,13 @@ def test_restore_matches_set_weight(tmp_path, precision):
     eng = StyleEngine(1, T, kw['cont_ids'], kw['style_ids'], precision=precision, device=dev)
     with pytest.raises(AstError, match='ae_dilatedconv_30/biases'):
         eng.restore(bad)
+    # the right element count in another layout: refused, as Saver.restore does
+    wrong = dict(W)
+    wrong['ae_dilatedconv_7/W'] = np.ascontiguousarray(W['ae_dilatedconv_7/W'].reshape(3, 128, 128))
+    bad2 = str(tmp_path / 'reshaped')
+    write_checkpoint(bad2, wrong)
+    with pytest.raises(AstError, match=r'ae_dilatedconv_7/W: checkpoint shape \[3,128,128\]'):
+        eng.restore(bad2)
     eng.close()
 
 
