@@ -18,7 +18,7 @@ RANGE_NONFINITE, RANGE_ACT, RANGE_GRAD, RANGE_TINY = 1, 2, 4, 8
 # Every symbol include/astyle.h declares (checked by tests/test_abi.py).
 EXPORTS = ('ast_create', 'ast_destroy', 'ast_workspace_bytes', 'ast_set_weight', 'ast_forward',
            'ast_get_extract', 'ast_embeds', 'ast_content_cols', 'ast_set_targets',
-           'ast_set_gamma', 'ast_loss_grad', 'ast_range_flags', 'ast_range_flags_reset', 'ast_set_cu_limit', 'ast_adam_step', 'ast_adam_step_dev',
+           'ast_set_gamma', 'ast_loss_grad', 'ast_loss_grad_phase', 'ast_range_flags', 'ast_range_flags_reset', 'ast_set_cu_limit', 'ast_adam_step', 'ast_adam_step_dev',
            'ast_lbfgs_workspace_bytes', 'ast_lbfgs_begin', 'ast_lbfgs_step', 'ast_lbfgs_state',
            'ast_timing', 'ast_timing_read', 'ast_ot_admm', 'ast_ckpt_open', 'ast_ckpt_close',
            'ast_ckpt_num_entries', 'ast_ckpt_entry', 'ast_ckpt_read_f32', 'ast_restore',
@@ -65,6 +65,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         'ast_set_targets': (i, [vp, vp, i, vp, i]),
         'ast_set_gamma': (i, [vp, f]),
         'ast_loss_grad': (i, [vp, vp, vp, vp, vp]),
+        'ast_loss_grad_phase': (i, [vp, vp, vp, vp, i, vp]),
         'ast_range_flags': (i, [vp, vp, vp]),
         'ast_range_flags_reset': (i, [vp, vp]),
         'ast_set_cu_limit': (i, [vp, i]),

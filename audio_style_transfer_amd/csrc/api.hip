@@ -96,6 +96,8 @@ struct ast_ctx {
     ast_cfg cfg;
     int dev = 0;
     int cus = 0;                            // persistent block kernels' workgroup budget (0 = every CU)
+    bool lg_front_done = false;             // ast_loss_grad_phase: phase 1 ran, phase 2 may follow
+    bool lg_top_max_done = false;           // (phase 1 -> 2) the Gram bwd recorded the chain's first max
     int nblk = 0;
     bool need_bott = false;
     int nu = 0, uid[32];
@@ -829,11 +831,10 @@ int ast_set_gamma(ast_ctx* x, float gamma) {
     return 0;
 }
 
-int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* stream) {
-    if (!x || !xd || !grad || !parts) return fail(AST_E_ARG, "null argument");
-    if (!x->targets) return fail(AST_E_STATE, "ast_set_targets has not been called");
-    (void)hipSetDevice(x->dev);
-    hipStream_t s = S(stream);
+// ast_loss_grad in two phases (ast_loss_grad_phase): the front runs the encoder forward, the
+// content taps and the Gram forward / style loss / Gram backward; the back runs the backward
+// chain through the blocks, d loss / d x, the loss parts, the STFT regulariser and the flags.
+static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
     const ast_cfg& c = x->cfg;
     tmark(x, s);
     int rc = run_forward(x, xd, s, true);
@@ -870,7 +871,8 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     }
     // style (methods.py:62-76, 118-119)
     tmark(x, s);
-    bool top_max_done = false;   // split: the Gram bwd recorded the top tensor's per-clip max
+    bool& top_max_done = x->lg_top_max_done;   // split: the Gram bwd recorded the top tensor's per-clip max
+    top_max_done = false;
     if (c.gatys) {
         GatysArgs g = gatys_args(x);
         launch_gatys_fwd(g, x->split ? 2 : (x->bf ? 1 : 0), s);
@@ -909,6 +911,14 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
         launch_gram_bwd_any(x, g, s);
     }
     tmark(x, s);
+    x->lg_front_done = true;
+    return 0;
+}
+
+static int loss_grad_back(ast_ctx* x, const float* xd, float* grad, float* parts, hipStream_t s) {
+    const ast_cfg& c = x->cfg;
+    const bool top_max_done = x->lg_top_max_done;
+    x->lg_front_done = false;
     // backward chain through the blocks
     auto direct = [&](int t) -> const void* {   // D_t: direct loss gradient of tensor t (or null)
         return x->tensor_in_style[t] ? (x->dgrad ? (const void*)((char*)x->dgrad + (size_t)t * x->tstride * x->esz) : tens(x, t)) : x->cg_buf[t];
@@ -1001,6 +1011,27 @@ int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* 
     if (x->timing && x->ev_used <= (int)x->ev.size()) x->timed_calls++;
     x->fwd_done = false;   // tapped tensors now hold their gradients, not activations
     return 0;
+}
+
+
+int ast_loss_grad(ast_ctx* x, const float* xd, float* grad, float* parts, void* stream) {
+    return ast_loss_grad_phase(x, xd, grad, parts, 0, stream);
+}
+
+int ast_loss_grad_phase(ast_ctx* x, const float* xd, float* grad, float* parts, int phase, void* stream) {
+    if (!x || !xd || ((phase == 0 || phase == 2) && (!grad || !parts))) return fail(AST_E_ARG, "null argument");
+    if (phase < 0 || phase > 2) return fail(AST_E_ARG, "phase must be 0 (both), 1 (front) or 2 (back)");
+    if (!x->targets) return fail(AST_E_STATE, "ast_set_targets has not been called");
+    (void)hipSetDevice(x->dev);
+    hipStream_t s = S(stream);
+    if (phase != 2) {
+        const int rc = loss_grad_front(x, xd, s);
+        if (rc) return rc;
+    } else if (!x->lg_front_done) {
+        return fail(AST_E_STATE, "ast_loss_grad_phase(2) needs phase 1 first");
+    }
+    if (phase == 1) return 0;
+    return loss_grad_back(x, xd, grad, parts, s);
 }
 
 int ast_range_flags(ast_ctx* x, int* flags, void* stream) {

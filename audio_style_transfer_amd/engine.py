@@ -185,6 +185,15 @@ class StyleEngine:
                                           self._ptr(parts), self._stream()))
         return parts, grad
 
+    def loss_grad_phase(self, x: torch.Tensor, grad: torch.Tensor, parts: torch.Tensor,
+                        phase: int) -> None:
+        """ast_loss_grad_phase: 1 = forward + Gram (fwd, style, bwd); 2 = the backward chain and
+        the rest (needs phase 1 of the same x first); 0 = both."""
+        if self._targets is None:
+            raise _lib.AstError('set_targets() first')
+        _lib.check(self.lib.ast_loss_grad_phase(self.h, self._ptr(self._x(x)), self._ptr(grad),
+                                                self._ptr(parts), int(phase), self._stream()))
+
     def adam_step(self, x, m, v, grad, step, lr=1.0, beta1=0.9, beta2=0.999, eps=1e-8):
         _lib.check(self.lib.ast_adam_step(self.h, self._ptr(x), self._ptr(m), self._ptr(v),
                                           self._ptr(grad), int(step), float(lr), float(beta1),
@@ -284,6 +293,95 @@ class AdamLoop:
         else:
             self._eager()
         return self.parts
+
+
+class AdamGroups:
+    """The throughput step over G disjoint clip groups on one GPU: one engine per group (its
+    persistent block kernels limited to 1/G of the CUs, ast_set_cu_limit), its own stream and
+    two captured graphs -- F = ast_loss_grad_phase 1 (encoder forward + Gram forward / style /
+    Gram backward) and R = phase 2 + Adam (the backward chain, d loss / d x, the update).  Group
+    0 replays F, R, F, R, ...; the other groups start one F ahead and replay R, F, R, F, ..., so
+    one group's HBM-bound Gram kernels (the end of F) run while another group's MFMA-bound block
+    kernels run on the other CUs.  Every step() is one full step of every group; the groups'
+    clips are independent, so each clip's trajectory is the one AdamLoop gives it alone."""
+
+    def __init__(self, engines, xs, lr=1.0, beta1=0.9, beta2=0.999, eps=1e-8):
+        self.engs, self.xs = list(engines), list(xs)
+        dev = self.xs[0].device
+        self.G = len(self.engs)
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        self.hp = (float(lr), float(beta1), float(beta2), float(eps))
+        self.m = [torch.zeros_like(x) for x in self.xs]
+        self.v = [torch.zeros_like(x) for x in self.xs]
+        self.grad = [torch.empty_like(x) for x in self.xs]
+        self.parts = [torch.empty(e.batch, 4, device=dev) for e in self.engs]
+        self.step_dev = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in self.engs]
+        self.streams = [torch.cuda.Stream(device=dev) for _ in self.engs]
+        self.graphs = []
+        for g, e in enumerate(self.engs):
+            if self.G > 1:
+                e.set_cu_limit(max(ncu // self.G, 1))
+            e.reset_range_flags()
+            self.graphs.append(self._capture(g))
+        self.primed = False
+
+    def _front(self, g):
+        self.engs[g].loss_grad_phase(self.xs[g], self.grad[g], self.parts[g], 1)
+
+    def _back(self, g):
+        e = self.engs[g]
+        e.loss_grad_phase(self.xs[g], self.grad[g], self.parts[g], 2)
+        e.adam_step_dev(self.xs[g], self.m[g], self.v[g], self.grad[g], self.step_dev[g], *self.hp)
+
+    def _capture(self, g):
+        st = (self.xs[g], self.m[g], self.v[g], self.step_dev[g])
+        saved = [t.clone() for t in st]
+        side = torch.cuda.Stream(device=self.xs[g].device)
+        side.wait_stream(torch.cuda.current_stream(self.xs[g].device))
+        with torch.cuda.stream(side):     # one eager step (allocator warm-up, as AdamLoop)
+            self._front(g)
+            self._back(g)
+        torch.cuda.current_stream(self.xs[g].device).wait_stream(side)
+        gf, gr = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gf):
+            self._front(g)
+        with torch.cuda.graph(gr):
+            self._back(g)
+        for t, s in zip(st, saved):
+            t.copy_(s)
+        self.engs[g].reset_range_flags()
+        return gf, gr
+
+    def step(self):
+        cur = torch.cuda.current_stream(self.xs[0].device)
+        for g in range(self.G):
+            self.streams[g].wait_stream(cur)
+            with torch.cuda.stream(self.streams[g]):
+                gf, gr = self.graphs[g]
+                if g == 0:
+                    gf.replay()
+                    gr.replay()
+                else:
+                    if not self.primed:
+                        gf.replay()
+                    gr.replay()
+                    gf.replay()
+        self.primed = True
+        for s in self.streams:
+            cur.wait_stream(s)
+
+    def finish(self):
+        """Complete the groups started one F ahead (their last F has no R yet): after this,
+        every group has taken the same number of full steps and parts / grad are current."""
+        if not self.primed:
+            return
+        cur = torch.cuda.current_stream(self.xs[0].device)
+        for g in range(1, self.G):
+            self.streams[g].wait_stream(cur)
+            with torch.cuda.stream(self.streams[g]):
+                self.graphs[g][1].replay()
+            cur.wait_stream(self.streams[g])
+        self.primed = False
 
 
 class LbfgsLoop:

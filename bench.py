@@ -61,6 +61,10 @@ def parse(argv=None):
     ap.add_argument('--gatys', action='store_true',
                     help='configs[4]: Gatys [L,128,128] Gram instead of the channel-wise one')
     ap.add_argument('--lr', type=float, default=2.0)
+    ap.add_argument('--groups', type=int, default=1,
+                    help='clip groups per GPU run concurrently (engine.AdamGroups: one engine, '
+                         'stream and 1/G of the CUs each, phase-shifted so one group\'s Gram '
+                         'kernels overlap another\'s block kernels); 1 = one engine')
     ap.add_argument('--graph', type=int, default=1,
                     help='1: replay the step from a captured HIP graph (default); 0: eager launches')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0,
@@ -135,25 +139,41 @@ def make_problem(eng, clips, T, dev):
     return torch.tensor(x0, device=dev)
 
 
-def run(args, Eng, precision, steps, warmup, ws, rank, dev, graph, clips=None, gatys=None):
-    """Build the engine, warm up, time `steps` steps (barrier + sync on both sides, max over
+def run(args, Eng, precision, steps, warmup, ws, rank, dev, graph, clips=None, gatys=None,
+        groups=1):
+    """Build the engine(s), warm up, time `steps` steps (barrier + sync on both sides, max over
     ranks).  A step is one AdamLoop step (ast_loss_grad + device-counter Adam), replayed from
-    a captured HIP graph when `graph`.  The per-kernel-family breakdown comes from HIP events
-    of 2 extra eager steps (events are not recorded inside a graph).  Returns (seconds,
-    engine timing dict, first loss, last loss, non-finite clips)."""
+    a captured HIP graph when `graph`; with groups > 1 one AdamGroups step (G engines of B / G
+    clips, phase-shifted on G streams: every clip still takes one full step).  The per-kernel-
+    family breakdown comes from HIP events of 2 extra eager steps of one engine (events are not
+    recorded inside a graph).  Returns (seconds, engine timing dict, first loss, last loss,
+    (non-finite clips, range-flagged clips), clips in the timed engine)."""
     import torch
-    from audio_style_transfer_amd.engine import AdamLoop
+    from audio_style_transfer_amd.engine import AdamGroups, AdamLoop
     from audio_style_transfer_amd.shard import clip_range, max_over_ranks
     B = clips or args.clips
     T = args.T
-    eng = Eng(B, T, [29], list(range(30)), precision=precision, device=dev, lambd=100.0,
-              gatys=args.gatys if gatys is None else gatys)
-    x = make_problem(eng, clip_range(ws * B, ws, rank), T, dev)
-    loop = AdamLoop(eng, x, lr=args.lr, graph=graph and dev.type == 'cuda')
+    G = groups if (groups > 1 and dev.type == 'cuda' and graph and B % groups == 0) else 1
+    mine = list(clip_range(ws * B, ws, rank))
+    Bg = B // G
+    engs, xs = [], []
+    for g in range(G):
+        e = Eng(Bg, T, [29], list(range(30)), precision=precision, device=dev, lambd=100.0,
+                gatys=args.gatys if gatys is None else gatys)
+        engs.append(e)
+        xs.append(make_problem(e, mine[g * Bg:(g + 1) * Bg], T, dev))
+    if G > 1:
+        loop = AdamGroups(engs, xs, lr=args.lr)
+        parts_of = lambda: torch.cat(loop.parts)
+        grad_of = lambda: torch.cat(loop.grad)
+    else:
+        loop = AdamLoop(engs[0], xs[0], lr=args.lr, graph=graph and dev.type == 'cuda')
+        parts_of = lambda: loop.parts
+        grad_of = lambda: loop.grad
     for _ in range(warmup):
         loop.step()
     sync(dev)
-    first_loss = loop.parts[:, 0].mean().item()
+    first_loss = parts_of()[:, 0].mean().item()
     barrier(ws)
     sync(dev)
     t0 = time.perf_counter()
@@ -163,24 +183,35 @@ def run(args, Eng, precision, steps, warmup, ws, rank, dev, graph, clips=None, g
     barrier(ws)
     el = time.perf_counter() - t0
     el = max_over_ranks(el, ws, device=dev)
-    last_loss = loop.parts[:, 0].mean().item()
+    if G > 1:
+        loop.finish()
+        sync(dev)
+    last_loss = parts_of()[:, 0].mean().item()
     # per-clip flag: the clip's loss parts or gradient hold a NaN / Inf (last step), and the
-    # clips whose range flags (sticky over every warm-up and timed step: AdamLoop resets them
-    # at its start) report an out-of-range or non-finite evaluation
-    bad = int((~torch.isfinite(loop.parts).all(dim=1) | ~torch.isfinite(loop.grad).all(dim=1)).sum().item())
-    flagged = int((eng.range_flags() & 7).ne(0).sum().item()) if dev.type == 'cuda' else 0
-    bad = (bad, flagged)
+    # clips whose range flags (sticky over every warm-up and timed step: the loops reset them
+    # at their start) report an out-of-range or non-finite evaluation
+    pp, gg = parts_of(), grad_of()
+    bad = int((~torch.isfinite(pp).all(dim=1) | ~torch.isfinite(gg).all(dim=1)).sum().item())
+    flagged = sum(int((e.range_flags() & 7).ne(0).sum().item()) for e in engs) if dev.type == 'cuda' else 0
+    eng = engs[0]
+    if G > 1:
+        eng.set_cu_limit(0)   # the breakdown: one engine's kernels with every CU
     eng.timing(True)
     for _ in range(2):
-        loop._eager()
+        if G > 1:
+            loop._front(0)
+            loop._back(0)
+        else:
+            loop._eager()
     sync(dev)
     tm = eng.timing_read()
     eng.timing(False)
-    del loop, x
-    eng.close()
+    del loop, xs
+    for e in engs:
+        e.close()
     if dev.type == 'cuda':
         torch.cuda.empty_cache()
-    return el, tm, first_loss, last_loss, bad
+    return el, tm, first_loss, last_loss, (bad, flagged), Bg
 
 
 def grad_check(Eng, precision, dev, gatys=False):
@@ -292,7 +323,7 @@ def lib_sha16():
 
 
 def block_roofline(precision, B, T, fwd_ms, bwd_ms, traffic, ms_per_step, gram_ms, L=30,
-                   nblk=30):
+                   nblk=30, B_step=None):
     """Roofline of the block kernels.  Per launch (all B clips): algorithmic bytes
     fwd = read e_l + write e_{l+1} (2A) + the relu-mask words (16 B per row written, 16 B of
     the previous layer's read); bwd = read the chain and D_l, write the chain (3A) + 32 B of
@@ -333,7 +364,7 @@ def block_roofline(precision, B, T, fwd_ms, bwd_ms, traffic, ms_per_step, gram_m
                     'PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, profiles/traffic.json, '
                     'null unless measured on this libastyle.so)' % (nblk * dom['launch_ms'],
                                                                       nblk * (fwd_ms + bwd_ms)))
-    step_bytes = nblk * (fbytes + bbytes) + 3 * L * A
+    step_bytes = (nblk * (fbytes + bbytes) + 3 * L * A) * (float(B_step or B) / B)
     roof['fwd'] = f
     roof['bwd'] = b
     roof['step'] = {'algorithmic_bytes': step_bytes, 'ms': ms_per_step,
@@ -349,14 +380,14 @@ def rank_main(args):
     ws, rank, dev = dist_setup(args)
     Eng = engine_class(args.engine)
     B, T, L = args.clips, args.T, 30
-    el, tm, first_loss, last_loss, bad = run(args, Eng, args.precision, args.steps, args.warmup,
-                                             ws, rank, dev, bool(args.graph))
+    el, tm, first_loss, last_loss, bad, Bt = run(args, Eng, args.precision, args.steps, args.warmup,
+                                                 ws, rank, dev, bool(args.graph), groups=args.groups)
     side = {}
     if ws == 1 and args.side_steps > 0 and dev.type == 'cuda':
         for p in ('fp32', 'bf16', 'split'):
             if p == args.precision:
                 continue
-            e2, tm2, _, _, _ = run(args, Eng, p, args.side_steps, 1, ws, rank, dev, bool(args.graph))
+            e2, tm2, _, _, _, _ = run(args, Eng, p, args.side_steps, 1, ws, rank, dev, bool(args.graph))
             calls = max(tm2['calls'], 1)
             side[p + '_mode'] = {'value': B * args.side_steps / 256.0 / e2, 'unit': 'iters/s',
                                  'steps': args.side_steps, 'precision': PREC_NOTE[p],
@@ -365,7 +396,7 @@ def rank_main(args):
                                                           'gram_fwd_ms', 'gram_bwd_ms', 'other_ms')},
                                  **grad_check(Eng, p, dev, args.gatys)}
         for p in ('split', 'fp32'):     # configs[1]: one 16384-sample clip
-            e1, _, _, _, _ = run(args, Eng, p, 10 * args.side_steps, 2, ws, rank, dev,
+            e1, _, _, _, _, _ = run(args, Eng, p, 10 * args.side_steps, 2, ws, rank, dev,
                                  bool(args.graph), clips=1, gatys=False)
             side['config1_%s' % p] = {'value': 10 * args.side_steps / e1, 'unit': 'iters/s',
                                       'note': 'configs[1]: 1 clip x %d, channel-wise Gram, 30 '
@@ -384,7 +415,7 @@ def rank_main(args):
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if (tj.get('precision') == args.precision and tj.get('clips') == B and tj.get('T') == T
+        if (tj.get('precision') == args.precision and tj.get('clips') == Bt and tj.get('T') == T
                 and tj.get('gatys', False) == args.gatys and tj.get('lib_sha16') == sha):
             traffic = {'fwd': tj['fwd_bytes_per_launch'], 'bwd': tj['bwd_bytes_per_launch'],
                        'gram_fwd': tj.get('gram_fwd_bytes_per_launch'),
@@ -393,7 +424,8 @@ def rank_main(args):
         traffic = None
     gram_fwd_ms = tm['gram_fwd_ms'] / calls
     gram_bwd_ms = tm['gram_bwd_ms'] / calls
-    gbytes = L * B * T * 128 * (2.0 if args.precision == 'bf16' else 4.0)
+    # the per-family breakdown is one engine's eager steps: Bt clips (B / groups)
+    gbytes = L * Bt * T * 128 * (2.0 if args.precision == 'bf16' else 4.0)
     out = {
         'metric': METRIC, 'value': value, 'unit': 'iters/s', 'n_gpus': ws, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': el / args.steps * 1e3,
@@ -406,10 +438,12 @@ def rank_main(args):
                                % (B, T) + 'L=30, cont_lyrs [29], lambd 100, gamma 0, Adam step',
                    'global_batch_clips': ws * B, 'T': T, 'parallelism': 'clip-sharded x%d' % ws,
                    'precision': args.precision, 'precision_detail': PREC_NOTE[args.precision],
-                   'hip_graph': bool(args.graph)},
+                   'hip_graph': bool(args.graph),
+                   'clip_groups': B // Bt,
+                   'breakdown_engine_clips': Bt},
         'clip_iters_per_s': value * 256.0,
-        'roofline': block_roofline(args.precision, B, T, fwd_ms, bwd_ms, traffic,
-                                   el / args.steps * 1e3, gram_fwd_ms + gram_bwd_ms),
+        'roofline': block_roofline(args.precision, Bt, T, fwd_ms, bwd_ms, traffic,
+                                   el / args.steps * 1e3, gram_fwd_ms + gram_bwd_ms, B_step=B),
         'lib_sha16': sha,
         'kernels_ms_per_step': {'block_fwd': tm['block_fwd_ms'] / calls,
                                 'block_bwd': tm['block_bwd_ms'] / calls,

@@ -96,6 +96,15 @@ int ast_set_targets(ast_ctx* ctx, const float* phi_c_dev, int phi_c_shared,
  * regulariser of methods.py:121-123 (0 when T < 1024: no full frame); like TF it is evaluated
  * whatever gamma is, and enters the gradient only through gamma. */
 int ast_loss_grad(ast_ctx* ctx, const float* x_dev, float* grad_dev, float* parts_dev, void* stream);
+/* ast_loss_grad in two stream-ordered phases: phase 1 = the encoder forward, the content taps and
+ * the Gram forward / style loss / Gram backward (grad_dev, parts_dev unused, may be NULL);
+ * phase 2 = the backward chain through the blocks, d loss / d x, the loss parts, the STFT
+ * regulariser and the range flags (needs phase 1 of the same x first: AST_E_STATE otherwise).
+ * phase 0 = both (= ast_loss_grad).  Lets contexts of disjoint clip groups run phase-shifted on
+ * separate streams (bench.py --groups): one group's HBM-bound Gram kernels overlap another's
+ * MFMA-bound block kernels.  Graph-capturable. */
+int ast_loss_grad_phase(ast_ctx* ctx, const float* x_dev, float* grad_dev, float* parts_dev,
+                        int phase, void* stream);
 
 /* Per-clip flags accumulated (OR) over every ast_loss_grad since the last reset, into flags_dev
  * [batch] (int, device) -- sticky, so an out-of-range line-search trial inside a device

@@ -357,3 +357,39 @@ def test_fused_content_tap_phi_at_buffer_end(weights, dev):
         for k in range(3):
             assert abs(out['split'][0][b, k] - out['fp32'][0][b, k]) <= 1e-4 * abs(out['fp32'][0][b, k]) + 1e-7, (b, k, out)
         assert rel(out['split'][1][b], out['fp32'][1][b]) <= 2e-3
+
+
+def test_loss_grad_phases_and_clip_groups(weights, dev):
+    """ast_loss_grad_phase: phase 1 + phase 2 equal ast_loss_grad bit for bit, and phase 2 alone
+    is refused.  engine.AdamGroups (two engines of 2 clips on half the CUs each, phase-shifted
+    graphs on two streams) leaves every clip where one AdamLoop over all 4 clips leaves it."""
+    from audio_style_transfer_amd._lib import AstError
+    from audio_style_transfer_amd.engine import AdamGroups, AdamLoop
+    T, B = 2048, 4
+    kw = CASES['ours']
+    x0 = torch.tensor(np.stack([O.mu_law_numpy(synthetic_clips(1, T, 300 + b)[0]) for b in range(B)]),
+                      dtype=torch.float32, device=dev)
+    eng = _engine(B, T, kw, weights)
+    _set(eng, 'ours', T, weights)
+    p0, g0 = eng.loss_grad(x0)
+    p1, g1 = torch.empty_like(p0), torch.empty_like(g0)
+    with pytest.raises(AstError, match='phase 1 first'):
+        eng.loss_grad_phase(x0, g1, p1, 2)
+    eng.loss_grad_phase(x0, g1, p1, 1)
+    eng.loss_grad_phase(x0, g1, p1, 2)
+    assert torch.equal(p0, p1) and torch.equal(g0, g1)
+    loop = AdamLoop(eng, x0.clone(), lr=1.0, graph=True)
+    for _ in range(3):
+        loop.step()
+    torch.cuda.synchronize()
+    ref = loop.x.clone()
+    engs = [_engine(2, T, kw, weights) for _ in range(2)]
+    for e in engs:
+        _set(e, 'ours', T, weights)
+    grp = AdamGroups(engs, [x0[:2].clone(), x0[2:].clone()], lr=1.0)
+    for _ in range(3):
+        grp.step()
+    grp.finish()
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(grp.xs), ref)
+    assert torch.equal(torch.cat(grp.parts), loop.parts)
