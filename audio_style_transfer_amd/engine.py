@@ -303,7 +303,9 @@ class AdamGroups:
     0 replays F, R, F, R, ...; the other groups start one F ahead and replay R, F, R, F, ..., so
     one group's HBM-bound Gram kernels (the end of F) run while another group's MFMA-bound block
     kernels run on the other CUs.  Every step() is one full step of every group; the groups'
-    clips are independent, so each clip's trajectory is the one AdamLoop gives it alone."""
+    clips are independent, so each clip's trajectory is the one AdamLoop gives it alone.  The
+    groups meet at the end of every step() (the current stream waits for them), so their phase
+    offset cannot drift."""
 
     def __init__(self, engines, xs, lr=1.0, beta1=0.9, beta2=0.999, eps=1e-8):
         self.engs, self.xs = list(engines), list(xs)
@@ -370,18 +372,8 @@ class AdamGroups:
         for s in self.streams:
             cur.wait_stream(s)
 
-    def finish(self):
-        """Complete the groups started one F ahead (their last F has no R yet): after this,
-        every group has taken the same number of full steps and parts / grad are current."""
-        if not self.primed:
-            return
-        cur = torch.cuda.current_stream(self.xs[0].device)
-        for g in range(1, self.G):
-            self.streams[g].wait_stream(cur)
-            with torch.cuda.stream(self.streams[g]):
-                self.graphs[g][1].replay()
-            cur.wait_stream(self.streams[g])
-        self.primed = False
+    # (after step(): x, parts and grad of every group are those of its last full step; the
+    #  groups started one F ahead hold the next step's F, which the next step() uses)
 
 
 class LbfgsLoop:

@@ -183,9 +183,6 @@ def run(args, Eng, precision, steps, warmup, ws, rank, dev, graph, clips=None, g
     barrier(ws)
     el = time.perf_counter() - t0
     el = max_over_ranks(el, ws, device=dev)
-    if G > 1:
-        loop.finish()
-        sync(dev)
     last_loss = parts_of()[:, 0].mean().item()
     # per-clip flag: the clip's loss parts or gradient hold a NaN / Inf (last step), and the
     # clips whose range flags (sticky over every warm-up and timed step: the loops reset them

@@ -389,7 +389,6 @@ def test_loss_grad_phases_and_clip_groups(weights, dev):
     grp = AdamGroups(engs, [x0[:2].clone(), x0[2:].clone()], lr=1.0)
     for _ in range(3):
         grp.step()
-    grp.finish()
     torch.cuda.synchronize()
     assert torch.equal(torch.cat(grp.xs), ref)
     assert torch.equal(torch.cat(grp.parts), loop.parts)
