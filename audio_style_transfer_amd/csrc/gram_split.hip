@@ -19,6 +19,7 @@
 //                             cg buffer, or the fused content tap computed here)
 // Loads and stores move whole 128-B lines (8 lanes x 16 B per row).
 #include "common.h"
+#include <cstdlib>
 
 namespace ast {
 namespace {
@@ -65,6 +66,9 @@ __device__ __forceinline__ void split8(const float4 (&v)[8], uint4& hi, uint4& l
 
 // forward.  Staging: thread (w, l) loads tensor u = 8 (w & 3) + (l & 7), channel quad l >> 3,
 // rows t0 + 8 (w >> 2) + k (k = 0..7): one load instruction covers 8 whole lines.
+// NST stages of loads in flight (2: 128 KiB per workgroup; 3: 192 KiB, the registers of a
+// third stage fit beside the accumulators at the same two waves per SIMD)
+template <int NST>
 __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
     __shared__ __attribute__((aligned(16))) u16 I[GCS * 32 * FRS];   // [c][u][hi t | lo t]
     int b, ch, c0;
@@ -83,8 +87,9 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
     for (int cc = 0; cc < 4; ++cc)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[cc][i] = 0.f;
-    // two stages of loads in flight (v0 / v1 alternate; tlen is a multiple of 2 GSS)
-    float4 v0[8], v1[8];
+    // NST stages of loads in flight (a ring of NST register sets; tlen is a multiple of 2 GSS)
+    float4 v[NST][8];
+    const int tend = tbeg + tlen;
     auto load = [&](float4 (&v)[8], int t0) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
@@ -95,7 +100,7 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
         split8<1>(v, fh[1], fl[1]);
         split8<2>(v, fh[2], fl[2]);
         split8<3>(v, fh[3], fl[3]);
-        if (t0 + 2 * GSS < tbeg + tlen) load(v, t0 + 2 * GSS);
+        if (t0 + NST * GSS < tend) load(v, t0 + NST * GSS);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -114,11 +119,13 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
             acc[cc] = mfma_bf16(xl, xh, acc[cc]);
         }
     };
-    load(v0, tbeg);
-    load(v1, tbeg + GSS);
-    for (int t0 = tbeg; t0 < tbeg + tlen; t0 += 2 * GSS) {
-        stage(v0, t0);
-        stage(v1, t0 + GSS);
+#pragma unroll
+    for (int q = 0; q < NST; ++q)
+        if (tbeg + q * GSS < tend) load(v[q], tbeg + q * GSS);
+    for (int t0 = tbeg; t0 < tend; t0 += NST * GSS) {
+#pragma unroll
+        for (int q = 0; q < NST; ++q)
+            if (t0 + q * GSS < tend) stage(v[q], t0 + q * GSS);
     }
 #pragma unroll
     for (int cc = 0; cc < 4; ++cc) {
@@ -502,8 +509,14 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_f(GramArgs a) {
 
 }  // namespace
 
+static int gram_stages() {   // ASTYLE_GRAM_STAGES=2 / 3 (A/B; default 3)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("ASTYLE_GRAM_STAGES"); v = e ? atoi(e) : 3; if (v != 2) v = 3; }
+    return v;
+}
 void launch_gram_fwd_s(const GramArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_gram_fwd_s, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+    if (gram_stages() == 2) hipLaunchKernelGGL(k_gram_fwd_s<2>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+    else hipLaunchKernelGGL(k_gram_fwd_s<3>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
 void launch_gram_fwd(const GramArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gram_fwd_f, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
