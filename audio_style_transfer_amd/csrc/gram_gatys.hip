@@ -336,8 +336,9 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     // staging: float4 f = tid + 256 k: row (tid >> 5) + 8 k, channels 4 (tid & 31) .. + 3
     const int c4 = tid & 31, r0 = tid >> 5;
-    float4 v[8];
-    auto load = [&](int k) {
+    // two stages of loads in flight (a ring of two register sets: 64 KiB per workgroup)
+    float4 vr[2][8];
+    auto load = [&](float4 (&v)[8], int k) {
         const float* src = E + (size_t)k * GYB * C + (size_t)r0 * C + 4 * c4;
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(src + (size_t)(8 * q) * C);
@@ -365,8 +366,7 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
     };
-    load(0);
-    for (int k = 0; k < nt; ++k) {
+    auto stage = [&](float4 (&v)[8], int k) {
         __syncthreads();   // the previous stage's fragment reads are done
 #pragma unroll
         for (int qq = 0; qq < 8; ++qq) {
@@ -377,7 +377,7 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
             *reinterpret_cast<uint2*>(&Lh[img(r)]) = make_uint2(h0, h1);
             *reinterpret_cast<uint2*>(&Ll[img(r)]) = make_uint2(l0, l1);
         }
-        if (k + 1 < nt) load(k + 1);      // next stage in flight during this one
+        if (k + 2 < nt) load(v, k + 2);   // two stages ahead
         __syncthreads();
 #pragma unroll
         for (int s = 0; s < GYB / 16; ++s) {
@@ -393,6 +393,12 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
                 mm3(acc[1], h0, l0, h2, l2);     // (X0, 3)
             }
         }
+    };
+    load(vr[0], 0);
+    if (1 < nt) load(vr[1], 1);
+    for (int k = 0; k < nt; k += 2) {
+        stage(vr[0], k);
+        if (k + 1 < nt) stage(vr[1], k + 1);
     }
     float* G = a.gpart + (((size_t)b * a.nchunk + ch) * a.nu + u) * (C * C);
     if (diag) {
