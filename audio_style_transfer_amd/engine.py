@@ -299,10 +299,11 @@ class AdamGroups:
     """The throughput step over G disjoint clip groups on one GPU: one engine per group (its
     persistent block kernels limited to 1/G of the CUs, ast_set_cu_limit), its own stream and
     two captured graphs -- F = ast_loss_grad_phase 1 (encoder forward + Gram forward / style /
-    Gram backward) and R = phase 2 + Adam (the backward chain, d loss / d x, the update).  Group
-    0 replays F, R, F, R, ...; the other groups start one F ahead and replay R, F, R, F, ..., so
+    Gram backward) and R = phase 2 + Adam (the backward chain, d loss / d x, the update).  Even
+    groups replay F, R, F, R, ...; odd groups start one F ahead and replay R, F, R, F, ..., so
     one group's HBM-bound Gram kernels (the end of F) run while another group's MFMA-bound block
-    kernels run on the other CUs.  Every step() is one full step of every group; the groups'
+    kernels run on the other CUs (even groups F, R; odd groups R, F).  Every step() is one full
+    step of every group; the groups'
     clips are independent, so each clip's trajectory is the one AdamLoop gives it alone.  The
     groups meet at the end of every step() (the current stream waits for them), so their phase
     offset cannot drift."""
@@ -360,7 +361,7 @@ class AdamGroups:
             self.streams[g].wait_stream(cur)
             with torch.cuda.stream(self.streams[g]):
                 gf, gr = self.graphs[g]
-                if g == 0:
+                if g % 2 == 0:
                     gf.replay()
                     gr.replay()
                 else:
