@@ -138,7 +138,10 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
 // backward.  Staging: thread (w, l) loads tensors 8 (w & 3) + k (k = 0..7), channel quad
 // l >> 3, row t0 + 8 (w >> 2) + (l & 7).  Output: 16 tensors at a time through O; padding
 // tensors (u >= nu) are neither read nor written.
-template <bool CONT>   // CONT: the fused content tap (a.cont_u >= 0); false: the round-2 kernel
+// CONT: the fused content tap (a.cont_u >= 0); false: the round-2 kernel.  NST stages of loads
+// in flight: 2 (the split of a stage into registers before the barrier) or 3 (each channel split
+// straight into the image after the barrier: 24 fewer live registers pay for the third stage)
+template <bool CONT, int NST>
 __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     __shared__ __attribute__((aligned(16))) u16 IH[GCS * GSS * BRS];       // [c][t][u] hi
     __shared__ __attribute__((aligned(16))) u16 IL[GCS * GSS * BRS];       // [c][t][u] lo
@@ -190,8 +193,8 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     const int cp_ = cit * GWT + tid, ctt = (cp_ >> 3) & 15, cq = cp_ & 7;
     const float* ce_src = CONT ? (const float*)a.act + (size_t)a.uid[a.cont_u & 31] * a.tstride + (size_t)b * a.T * C + c0 + 4 * cq : nullptr;
     const float* cp_src = CONT ? a.cont_phi + (size_t)b * a.cont_phi_bstride + a.cont_off + c0 + 4 * cq : nullptr;
-    // two stages of loads in flight (v0 / v1 alternate; tlen is a multiple of 2 GSS)
-    float4 v0[8], v1[8];
+    // NST stages of loads in flight (a ring of register sets; tlen is a multiple of 2 GSS)
+    float4 vr[NST][8];
     auto load = [&](float4 (&v)[8], int t0) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (lrs[k] ? lofs + (uint32_t)(t0 + st) * C : 0u));
@@ -205,37 +208,44 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
             if (c0 + 4 * cq < a.cont_ncol)
                 cph = *reinterpret_cast<const float4*>(cp_src + (size_t)(t0 + ctt) * a.cont_ncc);
         }
-        uint4 fh[4], fl[4];   // channel 4 sq + j: tensors 8 uo .. + 8 at row st, hi / lo
-        split8<0>(v, fh[0], fl[0]);
-        split8<1>(v, fh[1], fl[1]);
-        split8<2>(v, fh[2], fl[2]);
-        split8<3>(v, fh[3], fl[3]);
-        if (t0 + 2 * GSS < tend) load(v, t0 + 2 * GSS);
-        __syncthreads();   // the previous stage's image and O reads are done
+        if (NST == 2) {
+            uint4 fh[4], fl[4];   // channel 4 sq + j: tensors 8 uo .. + 8 at row st, hi / lo
+            split8<0>(v, fh[0], fl[0]);
+            split8<1>(v, fh[1], fl[1]);
+            split8<2>(v, fh[2], fl[2]);
+            split8<3>(v, fh[3], fl[3]);
+            if (t0 + NST * GSS < tend) load(v, t0 + NST * GSS);
+            __syncthreads();   // the previous stage's image and O reads are done
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int o = ((4 * sq + j) * GSS + st) * BRS + 8 * uo;
-            *reinterpret_cast<uint4*>(&IH[o]) = fh[j];
-            *reinterpret_cast<uint4*>(&IL[o]) = fl[j];
+            for (int j = 0; j < 4; ++j) {
+                const int o = ((4 * sq + j) * GSS + st) * BRS + 8 * uo;
+                *reinterpret_cast<uint4*>(&IH[o]) = fh[j];
+                *reinterpret_cast<uint4*>(&IL[o]) = fl[j];
+            }
+        } else {
+            __syncthreads();   // the previous stage's image and O reads are done
+            uint4 fh, fl;
+#define SPLIT_ONE(J) { split8<J>(v, fh, fl); const int o = ((4 * sq + J) * GSS + st) * BRS + 8 * uo; \
+                       *reinterpret_cast<uint4*>(&IH[o]) = fh; *reinterpret_cast<uint4*>(&IL[o]) = fl; }
+            SPLIT_ONE(0) SPLIT_ONE(1) SPLIT_ONE(2) SPLIT_ONE(3)
+#undef SPLIT_ONE
+            if (t0 + NST * GSS < tend) load(v, t0 + NST * GSS);
         }
         __syncthreads();
-        f32x4 acc[4][2];
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
+        // D_c = S~_c E_c of column half m for the wave's 4 channels (the B fragments re-read per
+        // half: only one half's accumulators are live)
+        auto dhalf = [&](int m, int cc) {
             const int o = ((4 * w + cc) * GSS + i16) * BRS + 8 * kq;
             const uint4 bh = *reinterpret_cast<const uint4*>(&IH[o]);
             const uint4 bl = *reinterpret_cast<const uint4*>(&IL[o]);
-#pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                f32x4 c = {0.f, 0.f, 0.f, 0.f};
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][0]),
-                                                           __builtin_bit_cast(bf16x8, bh), c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][1]),
-                                                           __builtin_bit_cast(bf16x8, bh), c, 0, 0, 0);
-                acc[cc][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][0]),
-                                                                    __builtin_bit_cast(bf16x8, bl), c, 0, 0, 0);
-            }
-        }
+            f32x4 c = {0.f, 0.f, 0.f, 0.f};
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][0]),
+                                                       __builtin_bit_cast(bf16x8, bh), c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][1]),
+                                                       __builtin_bit_cast(bf16x8, bh), c, 0, 0, 0);
+            return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][0]),
+                                                          __builtin_bit_cast(bf16x8, bl), c, 0, 0, 0);
+        };
         float4 cadd = make_float4(0.f, 0.f, 0.f, 0.f);
         if (CONT && cthr) {
             const int cc = c0 + 4 * cq;
@@ -251,12 +261,15 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
         // lane holds D_c[u = 16 m + 4 kq + i][t = i16] for the wave's 4 channels
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
+            f32x4 acc[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) acc[cc] = dhalf(m, cc);
             if (m) __syncthreads();   // the first half's O reads are done
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc)
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    O[((4 * kq + i) * GSS + i16) * ORS + 4 * w + cc] = acc[cc][m][i];
+                    O[((4 * kq + i) * GSS + i16) * ORS + 4 * w + cc] = acc[cc][i];
             __syncthreads();
             // 16 tensors x 16 rows x 8 quads = 2048 pieces, 4 per thread: u = 16 m + (p >> 7)
 #pragma unroll
@@ -280,11 +293,13 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
             }
         }
     };
-    load(v0, tbeg);
-    load(v1, tbeg + GSS);
-    for (int t0 = tbeg; t0 < tend; t0 += 2 * GSS) {
-        stage(v0, t0);
-        stage(v1, t0 + GSS);
+#pragma unroll
+    for (int q = 0; q < NST; ++q)
+        if (tbeg + q * GSS < tend) load(vr[q], tbeg + q * GSS);
+    for (int t0 = tbeg; t0 < tend; t0 += NST * GSS) {
+#pragma unroll
+        for (int q = 0; q < NST; ++q)
+            if (t0 + q * GSS < tend) stage(vr[q], t0 + q * GSS);
     }
     if (a.top_u >= 0) {   // one atomic per workgroup
         __shared__ float wm[GWT / 64];
@@ -509,6 +524,11 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_f(GramArgs a) {
 
 }  // namespace
 
+static int gram_bwd_stages() {   // ASTYLE_GRAM_BWD_STAGES=2 / 3 (A/B; default 2 until measured)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("ASTYLE_GRAM_BWD_STAGES"); v = e ? atoi(e) : 2; if (v != 3) v = 2; }
+    return v;
+}
 static int gram_stages() {   // ASTYLE_GRAM_STAGES=2 / 3 (A/B; default 3)
     static int v = -1;
     if (v < 0) { const char* e = getenv("ASTYLE_GRAM_STAGES"); v = e ? atoi(e) : 3; if (v != 2) v = 3; }
@@ -525,8 +545,14 @@ void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gram_bwd_f, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
 void launch_gram_bwd_s(const GramArgs& a, hipStream_t s) {
-    if (a.cont_u >= 0) hipLaunchKernelGGL(k_gram_bwd_s<true>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
-    else hipLaunchKernelGGL(k_gram_bwd_s<false>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+    const dim3 grid(a.B * a.nchunk * (C / GCS));
+    if (gram_bwd_stages() == 3) {
+        if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 3>), grid, dim3(GWT), 0, s, a);
+        else hipLaunchKernelGGL((k_gram_bwd_s<false, 3>), grid, dim3(GWT), 0, s, a);
+    } else {
+        if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 2>), grid, dim3(GWT), 0, s, a);
+        else hipLaunchKernelGGL((k_gram_bwd_s<false, 2>), grid, dim3(GWT), 0, s, a);
+    }
 }
 
 }  // namespace ast
