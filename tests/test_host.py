@@ -122,3 +122,29 @@ def test_stft_regularizer_matches_oracle():
         rv, rg = O.stft_reg(x[b])
         assert abs(float(val[b]) - rv) <= 1e-10 * abs(rv)
         assert np.linalg.norm(g[b].numpy() - rg) <= 1e-9 * np.linalg.norm(rg)
+
+
+def test_kaiser_best_resampler():
+    """utils.resample_kaiser_best restates librosa's default resampler (resampy 0.2 'kaiser_best'
+    + fix_length; parity unpinned: neither library is in the image): output length ceil(n r),
+    float32, channels independent, identity at equal rates, and a 440 Hz tone reproduced to
+    fp32 round-off for integer rate ratios (to 0.3 % at 44.1 -> 16 kHz, resampy's truncated
+    table step)."""
+    sr0 = 8000
+    t = np.arange(sr0) / sr0
+    x = np.sin(2 * np.pi * 440 * t).astype(np.float32)
+    assert utils.resample_kaiser_best(x, sr0, sr0) is not None
+    assert np.array_equal(utils.resample_kaiser_best(x, sr0, sr0), x)
+    for sr1, tol in ((16000, 1e-5), (4000, 1e-5)):
+        y = utils.resample_kaiser_best(x, sr0, sr1)
+        assert y.dtype == np.float32 and y.shape == (int(np.ceil(sr0 * sr1 / sr0)),)
+        ref = np.sin(2 * np.pi * 440 * np.arange(y.size) / sr1)
+        assert np.abs(y[200:-200] - ref[200:-200]).max() <= tol, sr1
+    x2 = np.stack([x, -0.25 * x])
+    y2 = utils.resample_kaiser_best(x2, sr0, 11025)
+    assert y2.shape == (2, int(np.ceil(sr0 * 11025 / sr0)))
+    assert np.array_equal(y2[0], utils.resample_kaiser_best(x, sr0, 11025))
+    y44 = utils.resample_kaiser_best(np.sin(2 * np.pi * 440 * np.arange(44100) / 44100).astype(np.float32), 44100, 16000)
+    assert y44.shape == (16000,)
+    ref = np.sin(2 * np.pi * 440 * np.arange(16000) / 16000)
+    assert np.abs(y44[300:-300] - ref[300:-300]).max() <= 4e-3
