@@ -1,3 +1,13 @@
+// TIMING PROBE (tools-only variant, results WRONG by design): the cost structure a Winograd
+// F(2,3) GEMM 1 would have inside this kernel's register and LDS budget -- GEMM 1 runs two of the
+// three tap groups (96 instead of 144 MFMAs per tile, as Winograd's four transformed products
+// over 32 output pairs), the conversion splits every unit a second time into the image row's
+// pad bytes (Winograd converts ~2x the rows: 128 transformed rows for 66 plain ones, each an
+// add + a split), and epilogue 1 adds the output transform's two adds per value.  The real
+// Winograd kernel would also need ~30 KB more LDS and ~10 more registers than this kernel has
+// (DESIGN.md §3), so this measures an upper bound of its gain.  ASTYLE_FWD_WINOPROBE=1 in the
+// libastyle_fwdvariants.so build.
+//
 // Split-fp16 encoder block forward (precision 2): model.py:95-116 for one block,
 //   u = dconv_d(relu(e_l)) + b_d        (masked.py:110-160, K = 3, SAME zero padding)
 //   e_{l+1} = e_l + W_r^T relu(u) + b_r
@@ -42,7 +52,7 @@ constexpr int LA = 2;                 // B-fragment lookahead (steps)
 // (e0_val: three samples per row, W0 / b0 of the lane's four channels in registers) instead of
 // loaded, so the start conv writes no e_0 tensor (model.py:82-93 folded into block 0)
 template <bool MASKED, bool ONESEG, bool XIN>
-__global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
+__global__ void __launch_bounds__(FT, 1) k_block_fwd_wp(FwdArgsS a, Layout ly) {
     __shared__ __attribute__((aligned(16))) uint8_t IMG[ISLOT];     // split relu(e_l) image
     __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];   // fp32 e_l (residual) rows
     __shared__ __attribute__((aligned(16))) uint8_t XV[TMS * RS];   // split v image
@@ -176,6 +186,13 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         uint8_t* p = IMG + imgo + 8 * k * RS;
         *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
         *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
+        {   // (probe) a transformed row's add + split, stored in the row's pad bytes
+            uint32_t g01, m01, g23, m23;
+            split2s((v.x + v.y) * sk, (v.y - v.x) * sk, g01, m01);
+            split2s((v.z + v.w) * sk, (v.w - v.z) * sk, g23, m23);
+            uint8_t* q = IMG + (lr + 8 * k) * RS + 512;
+            *reinterpret_cast<uint2*>(q) = make_uint2(g01 ^ m01, g23 ^ m23);
+        }
     };
 
     // e_{l+1} > 0 words of a finished tile -> next layer's positions (wave w: columns 16 w..)
@@ -266,10 +283,13 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
     auto epi1_part = [&](int j, int g, int part) {
         if (part == 0) {
             const float4 b4 = *reinterpret_cast<const float4*>(&BDS[chb + 8 * g]);
-            e1v.x = fmaxf(fmaf(acc1[j][4 * g + 0], a1, b4.x), 0.f);
-            e1v.y = fmaxf(fmaf(acc1[j][4 * g + 1], a1, b4.y), 0.f);
-            e1v.z = fmaxf(fmaf(acc1[j][4 * g + 2], a1, b4.z), 0.f);
-            e1v.w = fmaxf(fmaf(acc1[j][4 * g + 3], a1, b4.w), 0.f);
+            // (probe) the output transform's two adds per value
+            const float t0 = acc1[j][4 * g + 0] + acc1[j][4 * g + 1], t1 = acc1[j][4 * g + 1] - acc1[j][4 * g + 2];
+            const float t2 = acc1[j][4 * g + 2] + acc1[j][4 * g + 3], t3 = acc1[j][4 * g + 3] - acc1[j][4 * g + 0];
+            e1v.x = fmaxf(fmaf(acc1[j][4 * g + 0] + t0, a1, b4.x), 0.f);
+            e1v.y = fmaxf(fmaf(acc1[j][4 * g + 1] + t1, a1, b4.y), 0.f);
+            e1v.z = fmaxf(fmaf(acc1[j][4 * g + 2] + t2, a1, b4.z), 0.f);
+            e1v.w = fmaxf(fmaf(acc1[j][4 * g + 3] + t3, a1, b4.w), 0.f);
         } else {
             uint32_t h01, l01, h23, l23;
             split2(e1v.x, e1v.y, h01, l01);
@@ -318,7 +338,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
 #pragma unroll
         for (int q = 0; q < LA; ++q) bread(q, bh[q], bl[q]);
 #pragma unroll
-        for (int st = 0; st < 24; ++st) {
+        for (int st = 0; st < 16; ++st) {   // (probe) two tap groups: 96 MFMAs per tile
             const int tp = st >> 3, kb = st & 7, cb = st % (LA + 1);
             uint4 xh = bh[cb], xl = bl[cb];
             if (MASKED && ((tp == 0 && !ok0) || (tp == 2 && !ok2))) {
@@ -326,7 +346,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
                 xl = xh;
             }
             acc1[J] = mfma_f16(wd[tp][kb][0], xh, acc1[J]);
-            if (st + LA < 24) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
+            if (st + LA < 16) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
             side(st);
             acc1[J] = mfma_f16(wd[tp][kb][1], xh, acc1[J]);
             acc1[J] = mfma_f16(wd[tp][kb][0], xl, acc1[J]);
@@ -404,22 +424,32 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
         // A: GEMM 1 half 0 + epilogue 2 of the previous tile
         if (!FIRST) {
             epi2_begin();
-            gemm1h(J0{}, [&](int st) {
-                epi2_part(st / 3, st % 3, erp);
-                if (st >= 12 && st < 20) flush_part(0, (st - 12) >> 1, st & 1, erp);
-                if (st % 3 == 1 && st < 15) load_unit(nt, st / 3);   // rows of tile i+1: units 0..4
+            gemm1h(J0{}, [&](int st) {   // (probe: 16 steps carry the 24-step side work)
+#pragma unroll
+                for (int q = (3 * st) / 2; q < (3 * (st + 1)) / 2; ++q) {
+                    epi2_part(q / 3, q % 3, erp);
+                    if (q >= 12 && q < 20) flush_part(0, (q - 12) >> 1, q & 1, erp);
+                    if (q % 3 == 1 && q < 15) load_unit(nt, q / 3);
+                }
             }, cu);
             epi2_words();
             if (cu.b != prv.b) epi2_max();
         } else {
-            gemm1h(J0{}, [&](int st) { if (st % 3 == 1 && st < 15) load_unit(nt, st / 3); }, cu);
+            gemm1h(J0{}, [&](int st) {
+#pragma unroll
+                for (int q = (3 * st) / 2; q < (3 * (st + 1)) / 2; ++q)
+                    if (q % 3 == 1 && q < 15) load_unit(nt, q / 3);
+            }, cu);
         }
         STAMP(5)
         // B: GEMM 1 half 1 + epilogue 1 of half 0
         gemm1h(J1{}, [&](int st) {
-            if (st < 8) epi1_part(0, st >> 1, st & 1);
-            else if (!FIRST && st < 16) flush_part(1, (st - 8) >> 1, st & 1, erp);
-            if (st >= 11 && st % 3 == 2) load_unit(nt, 5 + (st - 11) / 3);   // units 5..8: 11 14 17 20
+#pragma unroll
+            for (int q = (3 * st) / 2; q < (3 * (st + 1)) / 2; ++q) {
+                if (q < 8) epi1_part(0, q >> 1, q & 1);
+                else if (!FIRST && q < 16) flush_part(1, (q - 8) >> 1, q & 1, erp);
+                if (q >= 11 && q % 3 == 2) load_unit(nt, 5 + (q - 11) / 3);
+            }
         }, cu);
         lds_barrier();   // v image half 0, u > 0 words half 0, e > 0 words of tile i-1
         STAMP(1)
@@ -468,22 +498,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
 
 }  // namespace
 
-#ifdef ASTYLE_FWD_VARIANTS
-// tools/variants/ build only (libastyle_fwdvariants.so): the measured-slower alternatives of this
-// kernel, bit-identical, selected by ASTYLE_FWD_ROLES=1 / ASTYLE_FWD_DB=1
-bool launch_block_fwd_roles(const FwdArgsS& a, hipStream_t s);   // tools/variants/block_fwd_roles.hip
-bool launch_block_fwd_db(const FwdArgsS& a, hipStream_t s);      // tools/variants/block_fwd_db.hip
-bool launch_block_fwd_winoprobe(const FwdArgsS& a, hipStream_t s);   // tools/variants/block_fwd_winoprobe.hip
-static bool env_on(const char* k) { const char* e = getenv(k); return e && atoi(e) != 0; }
-#endif
-
-void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
-#ifdef ASTYLE_FWD_VARIANTS
-    // (block 0 recomputes e_0 from x, which the variants do not: they run blocks 1..)
-    if (!a0.xin && env_on("ASTYLE_FWD_ROLES")) { launch_block_fwd_roles(a0, s); return; }
-    if (!a0.xin && env_on("ASTYLE_FWD_DB")) { launch_block_fwd_db(a0, s); return; }
-    if (env_on("ASTYLE_FWD_WINOPROBE")) { launch_block_fwd_winoprobe(a0, s); return; }
-#endif
+bool launch_block_fwd_winoprobe(const FwdArgsS& a0, hipStream_t s) {
     FwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
     a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));
@@ -491,22 +506,11 @@ void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
     const dim3 grid(std::min(nt, a.cus > 0 ? std::min(a.cus, sw::num_cus()) : sw::num_cus()));
     Layout ly;
     const bool masked = pick_layout(a.n, ly);
-    if (a.xin && (masked || ly.M != TMS || a.d != 1)) { fprintf(stderr, "block_fwd_s: xin needs d = 1\n"); abort(); }
-    if (masked) hipLaunchKernelGGL((k_block_fwd_s<true, false, false>), grid, dim3(FT), 0, s, a, ly);
-    else if (ly.M == TMS && a.xin) hipLaunchKernelGGL((k_block_fwd_s<false, true, true>), grid, dim3(FT), 0, s, a, ly);
-    else if (ly.M == TMS) hipLaunchKernelGGL((k_block_fwd_s<false, true, false>), grid, dim3(FT), 0, s, a, ly);
-    else hipLaunchKernelGGL((k_block_fwd_s<false, false, false>), grid, dim3(FT), 0, s, a, ly);
-}
-
-int sw::num_cus() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus <= 0) cus = 256;
-    }
-    return cus;
+    if (masked) hipLaunchKernelGGL((k_block_fwd_wp<true, false, false>), grid, dim3(FT), 0, s, a, ly);
+    else if (ly.M == TMS && a.xin) hipLaunchKernelGGL((k_block_fwd_wp<false, true, true>), grid, dim3(FT), 0, s, a, ly);
+    else if (ly.M == TMS) hipLaunchKernelGGL((k_block_fwd_wp<false, true, false>), grid, dim3(FT), 0, s, a, ly);
+    else hipLaunchKernelGGL((k_block_fwd_wp<false, false, false>), grid, dim3(FT), 0, s, a, ly);
+    return true;
 }
 
 }  // namespace ast
