@@ -17,7 +17,8 @@ SOURCES = ['encoder.hip', 'block_fwd_bf16.hip', 'block_bwd_bf16.hip', 'block_fwd
 # slower forward block kernels of round 3, selected at run time by
 # ASTYLE_FWD_ROLES=1 / ASTYLE_FWD_DB=1; never part of the shipped libastyle.so
 VARIANTS = os.path.join(os.path.dirname(PKG), 'tools', 'variants')
-VARIANT_SOURCES = {'fwdvariants': (['block_fwd_roles.hip', 'block_fwd_db.hip', 'block_fwd_winoprobe.hip'],
+VARIANT_SOURCES = {'fwdvariants': (['block_fwd_roles.hip', 'block_fwd_db.hip', 'block_fwd_winoprobe.hip',
+                                    'block_bwd_winoprobe.hip'],
                                    ['-DASTYLE_FWD_VARIANTS'])}
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 CXX = os.environ.get('CXX', 'g++')          # host-only sources (.cpp)
@@ -33,7 +34,7 @@ if os.environ.get('ASTYLE_NO_VGPR_FORM'):   # A/B builds: let the compiler place
     _CW = _CW[2:]
 EXTRA = {'block_fwd_bf16.hip': _CW, 'block_bwd_bf16.hip': _CW, 'block_fwd_split.hip': _CW,
          'block_bwd_split.hip': _CW, 'block_fwd_roles.hip': _CW, 'block_fwd_db.hip': _CW,
-         'block_fwd_winoprobe.hip': _CW}
+         'block_fwd_winoprobe.hip': _CW, 'block_bwd_winoprobe.hip': _CW}
 
 
 def _stale() -> bool:

@@ -1,3 +1,10 @@
+// TIMING PROBE (tools-only variant, results WRONG by design): the cost structure a Winograd
+// F(2,3) g_a (the transposed dilated conv) would have inside this kernel's budget -- g_a runs two
+// of the three tap groups (96 instead of 144 MFMAs per tile), every g_u image write is followed
+// by a second split of a transformed pair into the row's pad bytes, and the epilogue adds the
+// output transform's two adds per value.  An upper bound of Winograd's gain in the backward
+// (DESIGN.md §3).  ASTYLE_BWD_WINOPROBE=1 in the libastyle_fwdvariants.so build.
+//
 // Split-fp16 encoder block backward (precision 2): d loss / d e_l for one block of
 // model.py:95-116, restated by oracle/astyle_oracle.py:171-189 (encoder_backward):
 //   tot = d loss / d e_{l+1} (the chain, its own direct loss term included)
@@ -47,7 +54,7 @@ constexpr int LA = 2;                 // B-fragment lookahead (steps)
 // sum_c W0[k][c] out[t][c] over its 32 channels go to spart (launch_startx_gx sums the four
 // waves and forms d loss / d x): no 2 GiB g_0 round trip (model.py:82-93)
 template <bool MASKED, bool ONESEG, bool HAS_D, bool SX>
-__global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
+__global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
     __shared__ __attribute__((aligned(16))) uint8_t XS[ISLOT];        // split tot image
     __shared__ __attribute__((aligned(16))) uint8_t XG[GROWS * RS];   // split g_u image
     __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];     // fp32 tot + D_l rows
@@ -204,6 +211,12 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             uint8_t* p = XG + (J < 2 ? Lv[J] : Lhw) * RS + 2 * (chb + 8 * g);
             *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
             *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
+            {   // (probe) a transformed pair's add + split into the row's pad bytes
+                uint32_t g01, m01, g23, m23;
+                split2s((gq.x + gq.y) * f, (gq.y - gq.x) * f, g01, m01);
+                split2s((gq.z + gq.w) * f, (gq.w - gq.z) * f, g23, m23);
+                *reinterpret_cast<uint2*>(XG + (J < 2 ? Lv[J] : Lhw) * RS + 512) = make_uint2(g01 ^ m01, g23 ^ m23);
+            }
         }
     };
 
@@ -230,7 +243,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
 #pragma unroll
         for (int q = 0; q < LA; ++q) bread(q, bh[q], bl[q]);
 #pragma unroll
-        for (int st = 0; st < 24; ++st) {
+        for (int st = 0; st < 16; ++st) {   // (probe) two tap groups: 96 MFMAs per tile
             const int tp = st >> 3, kb = st & 7, cb = st % (LA + 1);
             uint4 xh = bh[cb], xl = bl[cb];
             if (MASKED && ((tp == 0 && !ok2) || (tp == 2 && !ok0))) {
@@ -238,8 +251,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
                 xl = xh;
             }
             acc2[J] = mfma_f16(wd[tp][kb][0], xh, acc2[J]);
-            if (st + LA < 24) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
-            side(st);
+            if (st + LA < 16) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
+#pragma unroll
+            for (int q = (3 * st) / 2; q < (3 * (st + 1)) / 2; ++q) side(q);   // (probe: all 24 steps' side work)
             acc2[J] = mfma_f16(wd[tp][kb][1], xh, acc2[J]);
             acc2[J] = mfma_f16(wd[tp][kb][0], xl, acc2[J]);
             step3_schedule();
@@ -264,10 +278,13 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         if (part == 0) {
             oe = *reinterpret_cast<const float4*>(er + Lc[J] * RS + 4 * (chb + 8 * g));
         } else if (part == 1) {
-            oo.x = fmaf(keep_if(acc2[J][4 * g + 0], mw, g), inv2, oe.x);
-            oo.y = fmaf(keep_if(acc2[J][4 * g + 1], mw, 4 + g), inv2, oe.y);
-            oo.z = fmaf(keep_if(acc2[J][4 * g + 2], mw, 8 + g), inv2, oe.z);
-            oo.w = fmaf(keep_if(acc2[J][4 * g + 3], mw, 12 + g), inv2, oe.w);
+            // (probe) the output transform's two adds per value
+            const float t0 = acc2[J][4 * g + 0] + acc2[J][4 * g + 1], t1 = acc2[J][4 * g + 1] - acc2[J][4 * g + 2];
+            const float t2 = acc2[J][4 * g + 2] + acc2[J][4 * g + 3], t3 = acc2[J][4 * g + 3] - acc2[J][4 * g + 0];
+            oo.x = fmaf(keep_if(acc2[J][4 * g + 0] + t0, mw, g), inv2, oe.x);
+            oo.y = fmaf(keep_if(acc2[J][4 * g + 1] + t1, mw, 4 + g), inv2, oe.y);
+            oo.z = fmaf(keep_if(acc2[J][4 * g + 2] + t2, mw, 8 + g), inv2, oe.z);
+            oo.w = fmaf(keep_if(acc2[J][4 * g + 3] + t3, mw, 12 + g), inv2, oe.w);
             if (SX) {
                 const float4 q0 = *reinterpret_cast<const float4*>(&W0S[chb + 8 * g]);
                 const float4 q1 = *reinterpret_cast<const float4*>(&W0S[C + chb + 8 * g]);
@@ -432,14 +449,7 @@ __global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, siz
 
 }  // namespace
 
-#ifdef ASTYLE_FWD_VARIANTS
-bool launch_block_bwd_winoprobe(const BwdArgsS& a, hipStream_t s);   // tools/variants/block_bwd_winoprobe.hip
-#endif
-
-void launch_block_bwd_s(const BwdArgsS& a0, hipStream_t s) {
-#ifdef ASTYLE_FWD_VARIANTS
-    { const char* e = getenv("ASTYLE_BWD_WINOPROBE"); if (e && atoi(e)) { launch_block_bwd_winoprobe(a0, s); return; } }
-#endif
+bool launch_block_bwd_winoprobe(const BwdArgsS& a0, hipStream_t s) {
     BwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
     a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));
@@ -448,8 +458,7 @@ void launch_block_bwd_s(const BwdArgsS& a0, hipStream_t s) {
     Layout ly;
     const bool masked = pick_layout(a.n, ly);
     const bool oneseg = !masked && ly.M == TMS;
-    if (a.spart && (!oneseg || a.dadd || a.d != 1)) { fprintf(stderr, "block_bwd_s: spart needs d = 1, no D\n"); abort(); }
-#define BWD_LAUNCH(M, O, D, X) hipLaunchKernelGGL((k_block_bwd_s<M, O, D, X>), grid, dim3(FT), 0, s, a, ly)
+#define BWD_LAUNCH(M, O, D, X) hipLaunchKernelGGL((k_block_bwd_wp<M, O, D, X>), grid, dim3(FT), 0, s, a, ly)
     if (masked) { if (a.dadd) BWD_LAUNCH(true, false, true, false); else BWD_LAUNCH(true, false, false, false); }
     else if (oneseg) {
         if (a.dadd) BWD_LAUNCH(false, true, true, false);
@@ -457,12 +466,7 @@ void launch_block_bwd_s(const BwdArgsS& a0, hipStream_t s) {
         else BWD_LAUNCH(false, true, false, false);
     } else { if (a.dadd) BWD_LAUNCH(false, false, true, false); else BWD_LAUNCH(false, false, false, false); }
 #undef BWD_LAUNCH
-}
-
-void launch_absmax(const float* x, size_t per_clip, int B, unsigned* out, hipStream_t s) {
-    int chunks = 1;
-    while (chunks < 64 && per_clip % ((size_t)chunks * 8) == 0 && per_clip / (chunks * 2) >= 4096) chunks *= 2;
-    hipLaunchKernelGGL(k_absmax, dim3(B * chunks), dim3(256), 0, s, x, per_clip, chunks, out);
+    return true;
 }
 
 }  // namespace ast
