@@ -14,6 +14,7 @@
 //        both operands so a lane's 8 k-steps walk one 128-B half row), C lands as 4
 //        consecutive channels per lane -> 8-B (bf16) / 16-B (fp32) stores of the same rows.
 #include "common.h"
+#include <cstdlib>
 
 namespace ast {
 
@@ -497,6 +498,98 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s(GatysArgs a) {
     }
 }
 
+// Split Gatys backward, round-4 form (ASTYLE_GATYS_BWD=2): v_mfma_f32_16x16x32_bf16 over
+// 16-row blocks, so a lane's E operand is 8 floats per k-step (32 registers a block) and three
+// blocks stay in flight (192 KiB per CU at two workgroups) instead of the 32x32 form's 64 floats
+// per lane and one block ahead at one wave per SIMD.  Per wave: rows t0 .. t0 + 127 in 8 blocks;
+// A = S~ (symmetric: S~[c][k] = S~[k][c]) split fragments from the LDS image, row c = 16 m + (l & 15),
+// k = 32 s + 8 (l >> 4) .. + 7; B = E split from registers, lane (n = l & 15, q = l >> 4): row
+// t + n, channels 32 s + 8 q .. + 7; D lane: row t + n, channels 16 m + 4 q .. + 3 (a float4).
+typedef float f32x4g __attribute__((ext_vector_type(4)));
+constexpr int GB2 = 3;   // blocks in flight
+__global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
+    __shared__ __attribute__((aligned(16))) u16 Sh[C * SBS];   // S~ hi
+    __shared__ __attribute__((aligned(16))) u16 Sl[C * SBS];   // S~ lo
+    const int tilesPer = a.T / GY_ROWS;
+    int bid = blockIdx.x;
+    const int tile = bid % tilesPer; bid /= tilesPer;
+    const int u = bid % a.nu, b = bid / a.nu;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float* S = a.smat + ((size_t)b * a.nu + u) * (C * C);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int i = tid + 256 * k, row = i >> 4, c8 = i & 15;   // 8 values per piece
+        const float4 x0 = *reinterpret_cast<const float4*>(S + row * C + c8 * 8);
+        const float4 x1 = *reinterpret_cast<const float4*>(S + row * C + c8 * 8 + 4);
+        uint32_t h[4], l[4];
+        split2g(x0.x, x0.y, h[0], l[0]);
+        split2g(x0.z, x0.w, h[1], l[1]);
+        split2g(x1.x, x1.y, h[2], l[2]);
+        split2g(x1.z, x1.w, h[3], l[3]);
+        *reinterpret_cast<uint4*>(&Sh[row * SBS + c8 * 8]) = make_uint4(h[0], h[1], h[2], h[3]);
+        *reinterpret_cast<uint4*>(&Sl[row * SBS + c8 * 8]) = make_uint4(l[0], l[1], l[2], l[3]);
+    }
+    const float* E = (const float*)a.act + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;
+    float* Ew = (float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;   // D (in place unless out of place)
+    const float* CG = (const float*)a.cg[u];
+    if (CG) CG += (size_t)b * a.T * C;
+    const int n = lane & 15, q = lane >> 4;
+    const int nblk = GY_ROWS / 4 / 16;
+    const int t0 = tile * GY_ROWS + w * (GY_ROWS / 4);
+    float4 vr[GB2][8];   // block in flight: k-step s, halves 0 / 1 at [2 s + hf]
+    auto load = [&](float4 (&v)[8], int blk) {
+        const float* src = E + (size_t)(t0 + 16 * blk + n) * C + 8 * q;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + 32 * (k >> 1) + 4 * (k & 1));
+    };
+    __syncthreads();
+    auto block = [&](float4 (&v)[8], int blk) {
+        asm volatile("" ::: "memory");   // S~ fragments are re-read from LDS per block, not hoisted
+        uint4 bh[4], bl[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            uint32_t h[4], l[4];
+            split2g(v[2 * s2].x, v[2 * s2].y, h[0], l[0]);
+            split2g(v[2 * s2].z, v[2 * s2].w, h[1], l[1]);
+            split2g(v[2 * s2 + 1].x, v[2 * s2 + 1].y, h[2], l[2]);
+            split2g(v[2 * s2 + 1].z, v[2 * s2 + 1].w, h[3], l[3]);
+            bh[s2] = make_uint4(h[0], h[1], h[2], h[3]);
+            bl[s2] = make_uint4(l[0], l[1], l[2], l[3]);
+        }
+        if (blk + GB2 < nblk) load(v, blk + GB2);
+        const int t = t0 + 16 * blk + n;
+        float* out = Ew + (size_t)t * C + 4 * q;
+        const float* cgr = CG ? CG + (size_t)t * C + 4 * q : nullptr;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            f32x4g c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const int o = (16 * m + n) * SBS + 32 * s2 + 8 * q;
+                const uint4 ah = *reinterpret_cast<const uint4*>(&Sh[o]);
+                const uint4 al = *reinterpret_cast<const uint4*>(&Sl[o]);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, bh[s2]), c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ah), __builtin_bit_cast(bf16x8, bl[s2]), c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al), __builtin_bit_cast(bf16x8, bh[s2]), c, 0, 0, 0);
+            }
+            float4 o4 = make_float4(c[0], c[1], c[2], c[3]);
+            if (cgr) {
+                const float4 cv = *reinterpret_cast<const float4*>(cgr + 16 * m);
+                o4.x += cv.x; o4.y += cv.y; o4.z += cv.z; o4.w += cv.w;
+            }
+            *reinterpret_cast<float4*>(out + 16 * m) = o4;
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < GB2; ++k)
+        if (k < nblk) load(vr[k], k);
+    for (int blk = 0; blk < nblk; blk += GB2) {
+#pragma unroll
+        for (int k = 0; k < GB2; ++k)
+            if (blk + k < nblk) block(vr[k], blk + k);
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // style loss: one workgroup per (clip, unique tensor); l2-normalise (methods.py:74), loss vs
 // phi (methods.py:118-119), d/dG through the normalisation, S~ = sum dG + dG^T.
@@ -587,7 +680,13 @@ void launch_gatys_fwd(const GatysArgs& a, int precision, hipStream_t s) {
 void launch_gatys_bwd(const GatysArgs& a, int precision, hipStream_t s) {
     const dim3 g(a.B * a.nu * (a.T / GY_ROWS));
     if (precision == 1) hipLaunchKernelGGL(k_gatys_bwd_bf16, g, dim3(256), 0, s, a);
-    else if (precision == 2) hipLaunchKernelGGL(k_gatys_bwd_s, g, dim3(256), 0, s, a);
+    else if (precision == 2) {
+        // ASTYLE_GATYS_BWD=2: the 16x16x32 three-blocks-in-flight form (A/B; read per call)
+        const char* e = getenv("ASTYLE_GATYS_BWD");
+        const int v = e ? atoi(e) : 1;
+        if (v == 2) hipLaunchKernelGGL(k_gatys_bwd_s2, g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(k_gatys_bwd_s, g, dim3(256), 0, s, a);
+    }
     else hipLaunchKernelGGL(k_gatys_bwd_f32, g, dim3(256), 0, s, a);
 }
 void launch_style_gatys(const GatysStyleArgs& a, hipStream_t s) {

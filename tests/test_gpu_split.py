@@ -392,3 +392,28 @@ def test_loss_grad_phases_and_clip_groups(weights, dev):
     torch.cuda.synchronize()
     assert torch.equal(torch.cat(grp.xs), ref)
     assert torch.equal(torch.cat(grp.parts), loop.parts)
+
+
+@pytest.mark.parametrize('form', ['1', '2'])
+def test_gatys_backward_forms(form, weights, golden, dev, monkeypatch):
+    """The split Gatys backward in both forms (ASTYLE_GATYS_BWD=1: 32x32x16, one block ahead;
+    2: 16x16x32, three 16-row blocks in flight) against the golden 'gatys' case at the fp32 bars,
+    and at B = 3 every slot equal to that clip alone."""
+    monkeypatch.setenv('ASTYLE_GATYS_BWD', form)
+    T = 2048
+    x = golden['gatys_x']
+    eng = _engine(1, T, CASES['gatys'], weights)
+    _set(eng, 'gatys', T, weights)
+    parts, grad = eng.loss_grad(torch.tensor(x[None], dtype=torch.float32, device=dev))
+    parts, grad = parts.cpu().numpy()[0], grad.cpu().numpy()[0]
+    ref_parts = golden['gatys_parts']
+    for k in range(4):
+        assert abs(parts[k] - ref_parts[k]) <= 1e-4 * abs(ref_parts[k]) + 1e-7, (form, k, parts, ref_parts)
+    e = rel(grad, golden['gatys_grad'])
+    print('gatys form %s: grad rel-L2 %.3g' % (form, e))
+    assert e <= 2e-3
+    xs = np.stack([x, x + 3.0, x - 5.0])
+    eng3 = _engine(3, T, CASES['gatys'], weights)
+    _set(eng3, 'gatys', T, weights)
+    p3, g3 = eng3.loss_grad(torch.tensor(xs, dtype=torch.float32, device=dev))
+    assert np.array_equal(p3.cpu().numpy()[0], parts) and np.array_equal(g3.cpu().numpy()[0], grad)
