@@ -324,6 +324,7 @@ __device__ __forceinline__ void store_tile(float* G, int I, int J, const f32x16&
 // the diagonal pairs {0, 1} / {2, 3} as (X0, X0), (X0, X1), (X1, X1); waves 2 / 3: block w - 2
 // against blocks 2 and 3) and the 6 off-diagonal ones are written twice: 30 instead of 48 MFMAs
 // per 16-row k-step and workgroup
+template <int NST>   // load stages in flight (2: 64 KiB per workgroup, 3: 96 KiB)
 __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
     __shared__ __attribute__((aligned(1024))) u16 Lh[GYB * C];   // [t][c] bf16 hi, swizzled
     __shared__ __attribute__((aligned(1024))) u16 Ll[GYB * C];   // lo
@@ -337,8 +338,8 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     // staging: float4 f = tid + 256 k: row (tid >> 5) + 8 k, channels 4 (tid & 31) .. + 3
     const int c4 = tid & 31, r0 = tid >> 5;
-    // two stages of loads in flight (a ring of two register sets: 64 KiB per workgroup)
-    float4 vr[2][8];
+    // NST stages of loads in flight (a ring of register sets)
+    float4 vr[NST][8];
     auto load = [&](float4 (&v)[8], int k) {
         const float* src = E + (size_t)k * GYB * C + (size_t)r0 * C + 4 * c4;
 #pragma unroll
@@ -378,7 +379,7 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
             *reinterpret_cast<uint2*>(&Lh[img(r)]) = make_uint2(h0, h1);
             *reinterpret_cast<uint2*>(&Ll[img(r)]) = make_uint2(l0, l1);
         }
-        if (k + 2 < nt) load(v, k + 2);   // two stages ahead
+        if (k + NST < nt) load(v, k + NST);   // NST stages ahead
         __syncthreads();
 #pragma unroll
         for (int s = 0; s < GYB / 16; ++s) {
@@ -395,11 +396,13 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
             }
         }
     };
-    load(vr[0], 0);
-    if (1 < nt) load(vr[1], 1);
-    for (int k = 0; k < nt; k += 2) {
-        stage(vr[0], k);
-        if (k + 1 < nt) stage(vr[1], k + 1);
+#pragma unroll
+    for (int q = 0; q < NST; ++q)
+        if (q < nt) load(vr[q], q);
+    for (int k = 0; k < nt; k += NST) {
+#pragma unroll
+        for (int q = 0; q < NST; ++q)
+            if (k + q < nt) stage(vr[q], k + q);
     }
     float* G = a.gpart + (((size_t)b * a.nchunk + ch) * a.nu + u) * (C * C);
     if (diag) {
@@ -674,7 +677,11 @@ __global__ void __launch_bounds__(256) k_style_gatys(GatysStyleArgs a) {
 void launch_gatys_fwd(const GatysArgs& a, int precision, hipStream_t s) {
     const dim3 g(a.B * a.nu * a.nchunk);
     if (precision == 1) hipLaunchKernelGGL(k_gatys_fwd_bf16, g, dim3(256), 0, s, a);
-    else if (precision == 2) hipLaunchKernelGGL(k_gatys_fwd_s, g, dim3(256), 0, s, a);
+    else if (precision == 2) {   // ASTYLE_GATYS_STAGES=3: three load stages in flight (A/B; default 2)
+        const char* e = getenv("ASTYLE_GATYS_STAGES");
+        if (e && atoi(e) == 3) hipLaunchKernelGGL(k_gatys_fwd_s<3>, g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(k_gatys_fwd_s<2>, g, dim3(256), 0, s, a);
+    }
     else hipLaunchKernelGGL(k_gatys_fwd_f32, g, dim3(256), 0, s, a);
 }
 void launch_gatys_bwd(const GatysArgs& a, int precision, hipStream_t s) {

@@ -394,12 +394,13 @@ def test_loss_grad_phases_and_clip_groups(weights, dev):
     assert torch.equal(torch.cat(grp.parts), loop.parts)
 
 
-@pytest.mark.parametrize('form', ['1', '2'])
+@pytest.mark.parametrize('form', ['1', '2', '3'])
 def test_gatys_backward_forms(form, weights, golden, dev, monkeypatch):
     """The split Gatys backward in both forms (ASTYLE_GATYS_BWD=1: 32x32x16, one block ahead;
     2: 16x16x32, three 16-row blocks in flight) against the golden 'gatys' case at the fp32 bars,
     and at B = 3 every slot equal to that clip alone."""
-    monkeypatch.setenv('ASTYLE_GATYS_BWD', form)
+    monkeypatch.setenv('ASTYLE_GATYS_BWD', '2' if form == '2' else '1')
+    monkeypatch.setenv('ASTYLE_GATYS_STAGES', '3' if form == '3' else '2')   # form 3: the forward's third stage
     T = 2048
     x = golden['gatys_x']
     eng = _engine(1, T, CASES['gatys'], weights)
