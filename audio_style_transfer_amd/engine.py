@@ -308,8 +308,9 @@ class AdamGroups:
     groups meet at the end of every step() (the current stream waits for them), so their phase
     offset cannot drift."""
 
-    def __init__(self, engines, xs, lr=1.0, beta1=0.9, beta2=0.999, eps=1e-8):
+    def __init__(self, engines, xs, lr=1.0, beta1=0.9, beta2=0.999, eps=1e-8, serial=False):
         self.engs, self.xs = list(engines), list(xs)
+        self.serial = bool(serial)   # diagnostics: every group's graphs on the current stream
         dev = self.xs[0].device
         self.G = len(self.engs)
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -359,7 +360,7 @@ class AdamGroups:
         cur = torch.cuda.current_stream(self.xs[0].device)
         for g in range(self.G):
             self.streams[g].wait_stream(cur)
-            with torch.cuda.stream(self.streams[g]):
+            with torch.cuda.stream(cur if self.serial else self.streams[g]):
                 gf, gr = self.graphs[g]
                 if g % 2 == 0:
                     gf.replay()
