@@ -135,6 +135,8 @@ struct ast_ctx {
     size_t gpart_elems = 0, smat_elems = 0; // per context (mode-dependent)
     int ncpart = 0;
     std::vector<void*> allocs;
+    struct Guard { char* base; size_t bytes; const char* name; };
+    std::vector<Guard> guards;              // ASTYLE_GUARD=1: guard bands around every buffer
     const float* phi_c = nullptr; int phi_c_shared = 0;
     const float* phi_s = nullptr; int phi_s_shared = 0;
     bool targets = false;
@@ -278,7 +280,26 @@ size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     return n;
 }
 
-int dalloc(ast_ctx* x, void** p, size_t bytes) {
+// ASTYLE_GUARD=1 (diagnostic): every buffer gets a GUARD_BYTES band of GUARD_FILL on both
+// sides; ast_debug_check_guards reports any band a kernel wrote into (out-of-bounds stores)
+constexpr size_t GUARD_BYTES = 64 << 10;
+constexpr int GUARD_FILL = 0x5a;
+static bool guard_on() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("ASTYLE_GUARD"); v = e && atoi(e) ? 1 : 0; }
+    return v == 1;
+}
+
+int dalloc(ast_ctx* x, void** p, size_t bytes, const char* name = "") {
+    if (guard_on()) {
+        char* base = nullptr;
+        HIPCHK(hipMalloc((void**)&base, bytes + 2 * GUARD_BYTES));
+        HIPCHK(hipMemset(base, GUARD_FILL, bytes + 2 * GUARD_BYTES));
+        x->allocs.push_back(base);
+        x->guards.push_back({base, bytes, name});
+        *p = base + GUARD_BYTES;
+        return 0;
+    }
     HIPCHK(hipMalloc(p, bytes));
     x->allocs.push_back(*p);
     return 0;
@@ -529,6 +550,40 @@ int ast_debug_stamps(void* dev_u64x16) {
     return 0;
 }
 
+// Diagnostic (ASTYLE_GUARD=1 contexts; not in astyle.h): device-synchronises, then checks every
+// buffer's guard bands; returns the number of buffers with a written band (-1: guards off) and
+// writes one line per such buffer to `report`.
+int ast_debug_check_guards(ast_ctx* x, char* report, int len) {
+    if (!x) return fail(AST_E_ARG, "null argument");
+    if (x->guards.empty()) return -1;
+    (void)hipSetDevice(x->dev);
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<unsigned char> h(GUARD_BYTES);
+    std::string rep;
+    int bad = 0;
+    for (const auto& g : x->guards) {
+        for (int side = 0; side < 2; ++side) {
+            const char* band = side ? g.base + GUARD_BYTES + g.bytes : g.base;
+            HIPCHK(hipMemcpy(h.data(), band, GUARD_BYTES, hipMemcpyDeviceToHost));
+            size_t first = GUARD_BYTES, last = 0, n = 0;
+            for (size_t i = 0; i < GUARD_BYTES; ++i)
+                if (h[i] != GUARD_FILL) { if (first == GUARD_BYTES) first = i; last = i; ++n; }
+            if (n) {
+                ++bad;
+                char line[256];
+                snprintf(line, sizeof(line), "%s (%zu bytes): %s band, %zu bytes written, offsets %lld..%lld from the buffer %s\n",
+                         g.name, g.bytes, side ? "upper" : "lower", n,
+                         side ? (long long)first : (long long)first - (long long)GUARD_BYTES,
+                         side ? (long long)last : (long long)last - (long long)GUARD_BYTES,
+                         side ? "end" : "start");
+                rep += line;
+            }
+        }
+    }
+    if (report && len > 0) snprintf(report, (size_t)len, "%s", rep.c_str());
+    return bad;
+}
+
 int ast_workspace_bytes(const ast_cfg* cfg, size_t* out) {
     if (!cfg || !out) return fail(AST_E_ARG, "null argument");
     ast_ctx tmp;
@@ -552,7 +607,7 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     const size_t BTC = (size_t)c.batch * c.T * C;
     x->tstride = BTC + tensor_pad();
     void* p;
-#define ALLOC(dst, bytes) do { if ((rc = dalloc(x, &p, (bytes)))) { ast_destroy(x); return rc; } dst = (decltype(dst))p; } while (0)
+#define ALLOC(dst, bytes) do { if ((rc = dalloc(x, &p, (bytes), #dst))) { ast_destroy(x); return rc; } dst = (decltype(dst))p; } while (0)
     x->bf = c.precision == 1;
     x->split = c.precision == 2;
     x->esz = x->bf ? 2 : 4;
