@@ -1,5 +1,5 @@
 """Diagnostic: which half of ast_loss_grad goes wrong on graph replay.  Against the eager result
-of the same x: (a) the whole call captured; (b) phase 1 captured, phase 2 eager; (c) phase 1
+of the same x: (a) the whole call captured; (b) both phases captured as two graphs; (c) phase 1
 eager, phase 2 captured; (d) the whole call with the block kernels on 128 CUs.  4 replays each.
 
   python tools/determinism2.py [B]"""
@@ -55,11 +55,12 @@ def main():
             e.set_cu_limit(0)
         elif mode == 'b':
             gr = capture(ph(1))
-            e.loss_grad_phase(x, g, p, 2)
+            g2 = capture(ph(2))
             for i in range(4):
                 gr.replay()
-                e.loss_grad_phase(x, g, p, 2)
+                g2.replay()
                 out.append(report('r%d' % i))
+            del g2
         else:
             e.loss_grad_phase(x, g, p, 1)
             gr = capture(ph(2))
