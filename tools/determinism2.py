@@ -13,18 +13,6 @@ import bench
 from audio_style_transfer_amd.engine import StyleEngine
 
 
-def capture(fn):
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        fn()
-    torch.cuda.current_stream().wait_stream(s)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        fn()
-    return g
-
-
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     dev = torch.device('cuda', 0)
@@ -43,27 +31,44 @@ def main():
                                                      dg.nonzero().flatten().tolist())
 
     ph = lambda k: (lambda: e.loss_grad_phase(x, g, p, k))
+    def warm(*fns):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for f in fns:
+                f()
+        torch.cuda.current_stream().wait_stream(s)
+
+    def cap(fn):
+        gg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gg):
+            fn()
+        return gg
+
     for mode in ('a', 'b', 'c', 'd'):
         out = []
         if mode in ('a', 'd'):
             if mode == 'd':
                 e.set_cu_limit(128)
-            gr = capture(ph(0))
+            warm(ph(0))
+            gr = cap(ph(0))
             for i in range(4):
                 gr.replay()
                 out.append(report('r%d' % i))
             e.set_cu_limit(0)
         elif mode == 'b':
-            gr = capture(ph(1))
-            g2 = capture(ph(2))
+            warm(ph(1), ph(2))
+            gr = cap(ph(1))
+            g2 = cap(ph(2))      # (the host side saw phase 1 captured just before)
             for i in range(4):
                 gr.replay()
                 g2.replay()
                 out.append(report('r%d' % i))
             del g2
         else:
+            warm(ph(1), ph(2))
             e.loss_grad_phase(x, g, p, 1)
-            gr = capture(ph(2))
+            gr = cap(ph(2))
             for i in range(4):
                 e.loss_grad_phase(x, g, p, 1)
                 gr.replay()
