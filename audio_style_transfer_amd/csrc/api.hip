@@ -319,7 +319,7 @@ void* tens(ast_ctx* x, int t) { return (char*)x->act + (size_t)t * x->tstride * 
 int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
     const ast_cfg& c = x->cfg;
     if (x->split) {
-        HIPCHK(hipMemsetAsync(x->gmax_e, 0, (size_t)(NBLK_MAX + 1) * c.batch * 4, s));
+        launch_zero32(x->gmax_e, (size_t)(NBLK_MAX + 1) * c.batch * 4, s);
         // e_0 is not stored: block 0 recomputes it from x (FwdArgsS::xin); masks and max only
         launch_startconv_fwd((const float*)xd, (float*)nullptr, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s,
                              (uint16_t*)x->me, x->gmax_e);
@@ -902,7 +902,7 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
     bool first_bott = true;
     const int fuse_u = fused_content_occ(x);
     if (fuse_u >= 0)   // the Gram backward writes nchunk x 4 of the occurrence's partial slots per clip
-        HIPCHK(hipMemsetAsync(x->cpart, 0, (size_t)c.batch * x->ncpart * 4, s));
+        launch_zero32(x->cpart, (size_t)c.batch * x->ncpart * 4, s);
     for (size_t i = 0; i < x->occ.size(); ++i) {
         if (fuse_u >= 0) break;
         const Occ& o = x->occ[i];
@@ -952,7 +952,7 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
         if (x->split && x->tensor_in_style[x->nblk]) {   // the chain's first max |tot| inside the Gram bwd
             for (int u = 0; u < x->nu; ++u) if (x->uid[u] == x->nblk) g.top_u = u;
             g.gmax_top = x->gmax_g + (size_t)x->nblk * c.batch;
-            HIPCHK(hipMemsetAsync(x->gmax_g, 0, (size_t)(NBLK_MAX + 1) * c.batch * 4, s));
+            launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s);
             top_max_done = g.top_u >= 0;
         }
         if (fuse_u >= 0) {
@@ -979,7 +979,7 @@ static int loss_grad_back(ast_ctx* x, const float* xd, float* grad, float* parts
         return x->tensor_in_style[t] ? (x->dgrad ? (const void*)((char*)x->dgrad + (size_t)t * x->tstride * x->esz) : tens(x, t)) : x->cg_buf[t];
     };
     if (x->split && !top_max_done) {
-        HIPCHK(hipMemsetAsync(x->gmax_g, 0, (size_t)(NBLK_MAX + 1) * c.batch * 4, s));
+        launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s);
         const void* top = direct(x->nblk);
         if (!top) return fail(AST_E_STATE, "top block has no loss gradient");
         launch_absmax((const float*)top, (size_t)c.T * C, c.batch, x->gmax_g + (size_t)x->nblk * c.batch, s);
@@ -1104,7 +1104,7 @@ int ast_set_cu_limit(ast_ctx* x, int cus) {
 
 int ast_range_flags_reset(ast_ctx* x, void* stream) {
     if (!x) return fail(AST_E_ARG, "null argument");
-    HIPCHK(hipMemsetAsync(x->rflags, 0, (size_t)x->cfg.batch * 4, S(stream)));
+    launch_zero32(x->rflags, (size_t)x->cfg.batch * 4, S(stream));
     return 0;
 }
 
@@ -1142,7 +1142,7 @@ int ast_lbfgs_begin(ast_ctx* x, void* ws, float* xd, const double* x0, const int
         return fail(AST_E_STATE, "continuing (x0 NULL) needs a workspace started with x0");
     if (x0 && !known) x->lb_ws.push_back(ws);
     // a new epoch: the range flags accumulate over its evaluations (include/astyle.h)
-    HIPCHK(hipMemsetAsync(x->rflags, 0, (size_t)x->cfg.batch * 4, S(stream)));
+    launch_zero32(x->rflags, (size_t)x->cfg.batch * 4, S(stream));
     launch_lbfgs_begin(ws, xd, x0, active, x->cfg.batch, x->cfg.T, m, maxiter, maxls, ftol, gtol,
                        S(stream));
     HIPCHK(hipGetLastError());

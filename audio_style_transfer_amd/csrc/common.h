@@ -302,6 +302,7 @@ void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b
                           int B, int T, hipStream_t s, uint16_t* me0 = nullptr,
                           unsigned* gmax = nullptr);
 void launch_startx_gx(const float* spart, float* gx, int B, int T, hipStream_t s);
+void launch_zero32(void* p, size_t bytes, hipStream_t s);   // bytes: a multiple of 4
 template <typename S>
 void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T,
                           hipStream_t s);

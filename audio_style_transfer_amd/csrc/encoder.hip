@@ -8,6 +8,7 @@
 // TM+2 input rows in LDS once, and runs both GEMMs (K = 3*128 then 128) on
 // v_mfma_f32_32x32x2_f32 with fp32 accumulation; the bias/relu/residual/mask epilogues are
 // fused and the relu masks leave as bits (16 B per row) for the backward.
+#include <algorithm>
 #include "common.h"
 
 namespace ast {
@@ -473,6 +474,17 @@ void launch_bottleneck_bwd(const float* gy, S* ge, const float* wb, int accumula
     const size_t n = (size_t)B * T * C;
     hipLaunchKernelGGL(k_bottleneck_bwd<S>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                        gy, ge, wb, accumulate, B, T);
+}
+// zero fill of n 32-bit words: the per-call clears of the max / partial-sum / flag buffers as
+// kernel nodes (a graph replay then orders them like every other node: no memset nodes)
+__global__ void __launch_bounds__(256) k_zero32(uint32_t* __restrict__ p, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) p[i] = 0u;
+}
+void launch_zero32(void* p, size_t bytes, hipStream_t s) {
+    const size_t n = bytes / 4;
+    if (!n) return;
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_zero32, dim3(blocks), dim3(256), 0, s, (uint32_t*)p, n);
 }
 void launch_to_f32(const u16* src, float* dst, size_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_to_f32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, n);
