@@ -16,6 +16,12 @@ __global__ void bump(int* iter) { if (threadIdx.x == 0 && blockIdx.x == 0) iter[
 __global__ void produce(float* buf, const int* iter) {
     buf[blockIdx.x * NT + threadIdx.x] = (float)(iter[0] * 1000 + (int)blockIdx.x);
 }
+__global__ void kmax(unsigned* gmax, const int* iter) {   // per-clip max, clip = blockIdx % 8
+    if (threadIdx.x == 0) atomicMax(gmax + blockIdx.x % 8, (unsigned)(iter[0] * 1000 + (int)blockIdx.x % 8));
+}
+__global__ void kuse(const unsigned* gmax, float* out) {
+    out[blockIdx.x * NT + threadIdx.x] = (float)gmax[(blockIdx.x + 3) % 8];
+}
 __global__ void consume(const float* buf, float* out) {
     const int src = (blockIdx.x + 1) % NB;
     out[blockIdx.x * NT + threadIdx.x] = buf[src * NT + threadIdx.x];
@@ -65,6 +71,44 @@ int main() {
     }
     printf("RESULT eager launches with stale data: %d / 4, graph replays with stale data: %d / 6\n",
            bad_eager, bad_graph);
+    // second pattern: hipMemsetAsync clear -> atomicMax per clip -> readers of another clip's max
+    unsigned* gmax;
+    CK(hipMalloc(&gmax, 32));
+    auto check2 = [&](int itv, const char* tag, int k) {
+        std::vector<float> h(NB * NT);
+        if (hipMemcpy(h.data(), out, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        int bad = 0, first = -1;
+        for (int gi = 0; gi < NB; ++gi)
+            if (h[gi * NT] != (float)(itv * 1000 + (gi + 3) % 8)) { if (first < 0) first = gi; ++bad; }
+        printf("%s %d: iter %d, %d stale rows (first row %d: %g)\n", tag, k, itv, bad, first, first >= 0 ? h[first * NT] : 0.0);
+        return bad;
+    };
+    int b2e = 0, b2g = 0;
+    for (int k = 0; k < 3; ++k) {
+        hipLaunchKernelGGL(bump, dim3(1), dim3(64), 0, s, iter);
+        CK(hipMemsetAsync(gmax, 0, 32, s));
+        hipLaunchKernelGGL(kmax, dim3(NB), dim3(64), 0, s, gmax, iter);
+        hipLaunchKernelGGL(kuse, dim3(NB), dim3(NT), 0, s, gmax, out);
+        CK(hipStreamSynchronize(s));
+        b2e += check2(++it, "memset+max eager", k) != 0;
+    }
+    hipGraph_t g2;
+    hipGraphExec_t ge2;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    hipLaunchKernelGGL(bump, dim3(1), dim3(64), 0, s, iter);
+    CK(hipMemsetAsync(gmax, 0, 32, s));
+    hipLaunchKernelGGL(kmax, dim3(NB), dim3(64), 0, s, gmax, iter);
+    hipLaunchKernelGGL(kuse, dim3(NB), dim3(NT), 0, s, gmax, out);
+    CK(hipStreamEndCapture(s, &g2));
+    CK(hipGraphInstantiate(&ge2, g2, nullptr, nullptr, 0));
+    for (int k = 0; k < 6; ++k) {
+        CK(hipGraphLaunch(ge2, s));
+        CK(hipStreamSynchronize(s));
+        b2g += check2(++it, "memset+max graph replay", k) != 0;
+    }
+    printf("RESULT memset+atomicMax: eager launches wrong: %d / 3, graph replays wrong: %d / 6\n", b2e, b2g);
+    CK(hipGraphExecDestroy(ge2));
+    CK(hipGraphDestroy(g2));
     CK(hipGraphExecDestroy(ge));
     CK(hipGraphDestroy(g));
     CK(hipStreamDestroy(s));
