@@ -17,7 +17,7 @@ __global__ void produce(float* buf, const int* iter) {
     buf[blockIdx.x * NT + threadIdx.x] = (float)(iter[0] * 1000 + (int)blockIdx.x);
 }
 __global__ void kmax(unsigned* gmax, const int* iter) {   // per-clip max, clip = blockIdx % 8
-    if (threadIdx.x == 0) atomicMax(gmax + blockIdx.x % 8, (unsigned)(iter[0] * 1000 + (int)blockIdx.x % 8));
+    if (threadIdx.x == 0) atomicMax(gmax + blockIdx.x % 8, (unsigned)(1000000 - iter[0] * 1000 + (int)blockIdx.x % 8));   // decreasing: a missed clear keeps an old max
 }
 __global__ void kuse(const unsigned* gmax, float* out) {
     out[blockIdx.x * NT + threadIdx.x] = (float)gmax[(blockIdx.x + 3) % 8];
@@ -79,7 +79,7 @@ int main() {
         if (hipMemcpy(h.data(), out, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
         int bad = 0, first = -1;
         for (int gi = 0; gi < NB; ++gi)
-            if (h[gi * NT] != (float)(itv * 1000 + (gi + 3) % 8)) { if (first < 0) first = gi; ++bad; }
+            if (h[gi * NT] != (float)(1000000 - itv * 1000 + (gi + 3) % 8)) { if (first < 0) first = gi; ++bad; }
         printf("%s %d: iter %d, %d stale rows (first row %d: %g)\n", tag, k, itv, bad, first, first >= 0 ? h[first * NT] : 0.0);
         return bad;
     };
