@@ -101,10 +101,17 @@ int main() {
     hipLaunchKernelGGL(kuse, dim3(NB), dim3(NT), 0, s, gmax, out);
     CK(hipStreamEndCapture(s, &g2));
     CK(hipGraphInstantiate(&ge2, g2, nullptr, nullptr, 0));
+    float* junk;
+    CK(hipMalloc(&junk, NB * NT * 4));
     for (int k = 0; k < 6; ++k) {
         CK(hipGraphLaunch(ge2, s));
         CK(hipStreamSynchronize(s));
         b2g += check2(++it, "memset+max graph replay", k) != 0;
+        if (k >= 2) {   // eager work between replays: a memset of another buffer and a kernel
+            CK(hipMemsetAsync(junk, 0x7f, 4096, s));
+            hipLaunchKernelGGL(consume, dim3(NB), dim3(NT), 0, s, buf, junk);
+            CK(hipStreamSynchronize(s));
+        }
     }
     printf("RESULT memset+atomicMax: eager launches wrong: %d / 3, graph replays wrong: %d / 6\n", b2e, b2g);
     CK(hipGraphExecDestroy(ge2));
