@@ -501,7 +501,7 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s(GatysArgs a) {
     }
 }
 
-// Split Gatys backward, round-4 form (ASTYLE_GATYS_BWD=2): v_mfma_f32_16x16x32_bf16 over
+// Split Gatys backward, round-4 form (the default; ASTYLE_GATYS_BWD=1 the 32x32 form): v_mfma_f32_16x16x32_bf16 over
 // 16-row blocks, so a lane's E operand is 8 floats per k-step (32 registers a block) and three
 // blocks stay in flight (192 KiB per CU at two workgroups) instead of the 32x32 form's 64 floats
 // per lane and one block ahead at one wave per SIMD.  Per wave: rows t0 .. t0 + 127 in 8 blocks;
@@ -688,11 +688,12 @@ void launch_gatys_bwd(const GatysArgs& a, int precision, hipStream_t s) {
     const dim3 g(a.B * a.nu * (a.T / GY_ROWS));
     if (precision == 1) hipLaunchKernelGGL(k_gatys_bwd_bf16, g, dim3(256), 0, s, a);
     else if (precision == 2) {
-        // ASTYLE_GATYS_BWD=2: the 16x16x32 three-blocks-in-flight form (A/B; read per call)
+        // default: the 16x16x32 three-blocks-in-flight form (round 4: 23.9 vs 28.2 ms per call
+        // at 256 clips); ASTYLE_GATYS_BWD=1 selects the 32x32x16 form (A/B; read per call)
         const char* e = getenv("ASTYLE_GATYS_BWD");
-        const int v = e ? atoi(e) : 1;
-        if (v == 2) hipLaunchKernelGGL(k_gatys_bwd_s2, g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(k_gatys_bwd_s, g, dim3(256), 0, s, a);
+        const int v = e ? atoi(e) : 2;
+        if (v == 1) hipLaunchKernelGGL(k_gatys_bwd_s, g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(k_gatys_bwd_s2, g, dim3(256), 0, s, a);
     }
     else hipLaunchKernelGGL(k_gatys_bwd_f32, g, dim3(256), 0, s, a);
 }

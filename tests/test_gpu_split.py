@@ -253,6 +253,45 @@ def test_split_graph_replay_matches_eager(weights, dev):
     assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
 
 
+def test_graph_replays_bitwise_at_bench_length(dev):
+    """Every replay of a captured ast_loss_grad equals the eager call bit for bit, at the bench's
+    clip length with 8 clips (one per XCD in the block kernels' tile order), with eager work
+    between replays, and two engines' graphs interleaved.  (With hipMemsetAsync nodes for the
+    per-call clears, replays after the first differed on 2 of 8 clips under the HIP runtime's
+    graph packet capture: DESIGN.md §12.)"""
+    import bench
+    from audio_style_transfer_amd.engine import StyleEngine
+    B, T = 8, 16384
+    engs, xs, refs, outs, graphs = [], [], [], [], []
+    for g in range(2):
+        e = StyleEngine(B, T, [29], list(range(30)), precision='split', device=dev, lambd=100.0)
+        x = bench.make_problem(e, list(range(g * B, (g + 1) * B)), T, dev)
+        p, gr = e.loss_grad(x)
+        engs.append(e)
+        xs.append(x)
+        refs.append((p.clone(), gr.clone()))
+    for e, x in zip(engs, xs):
+        p, gr = torch.empty(B, 4, device=dev), torch.empty_like(x)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            e.loss_grad(x, gr, p)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            e.loss_grad(x, gr, p)
+        outs.append((p, gr))
+        graphs.append(graph)
+    for _ in range(3):
+        for k in range(2):
+            graphs[k].replay()
+            torch.cuda.synchronize()
+            assert torch.equal(outs[k][0], refs[k][0]) and torch.equal(outs[k][1], refs[k][1])
+            engs[k].range_flags()   # eager library work between replays
+    for e in engs:
+        e.close()
+
+
 def test_split_scale_range(weights, dev):
     """The power-of-two operand scales (splitwave.h) make the split path independent of the
     input's magnitude: the reference's initial point x = 1e-6 (methods.py:49-54, activations
@@ -397,7 +436,7 @@ def test_loss_grad_phases_and_clip_groups(weights, dev):
 @pytest.mark.parametrize('form', ['1', '2', '3'])
 def test_gatys_backward_forms(form, weights, golden, dev, monkeypatch):
     """The split Gatys backward in both forms (ASTYLE_GATYS_BWD=1: 32x32x16, one block ahead;
-    2: 16x16x32, three 16-row blocks in flight) against the golden 'gatys' case at the fp32 bars,
+    2, the default: 16x16x32, three 16-row blocks in flight) against the golden 'gatys' case at the fp32 bars,
     and at B = 3 every slot equal to that clip alone."""
     monkeypatch.setenv('ASTYLE_GATYS_BWD', '2' if form == '2' else '1')
     monkeypatch.setenv('ASTYLE_GATYS_STAGES', '3' if form == '3' else '2')   # form 3: the forward's third stage
