@@ -141,7 +141,8 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
 // CONT: the fused content tap (a.cont_u >= 0); false: the round-2 kernel.  NST stages of loads
 // in flight: 2 (the split of a stage into registers before the barrier) or 3 (each channel split
 // straight into the image after the barrier: 24 fewer live registers pay for the third stage)
-template <bool CONT, int NST>
+// NTM (A/B, ASTYLE_GRAM_NT): bit 0 nontemporal staging loads of E, bit 1 nontemporal D stores
+template <bool CONT, int NST, int NTM = 0>
 __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     __shared__ __attribute__((aligned(16))) u16 IH[GCS * GSS * BRS];       // [c][t][u] hi
     __shared__ __attribute__((aligned(16))) u16 IL[GCS * GSS * BRS];       // [c][t][u] lo
@@ -197,7 +198,13 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     float4 vr[NST][8];
     auto load = [&](float4 (&v)[8], int t0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (lrs[k] ? lofs + (uint32_t)(t0 + st) * C : 0u));
+        for (int k = 0; k < 8; ++k) {
+            const float4* src = reinterpret_cast<const float4*>(ld[k] + (lrs[k] ? lofs + (uint32_t)(t0 + st) * C : 0u));
+            if (NTM & 1) {
+                const f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src));
+                v[k] = make_float4(q[0], q[1], q[2], q[3]);
+            } else v[k] = *src;
+        }
     };
     auto stage = [&](float4 (&v)[8], int t0) {
         float4 ce, cph = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -286,7 +293,8 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
                         o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
                     }
                     if (CONT && u == a.cont_u) { o.x += cadd.x; o.y += cadd.y; o.z += cadd.z; o.w += cadd.w; }
-                    *reinterpret_cast<float4*>((float*)a.actw + off) = o;
+                    if (NTM & 2) __builtin_nontemporal_store(f32x4{o.x, o.y, o.z, o.w}, reinterpret_cast<f32x4*>((float*)a.actw + off));
+                    else *reinterpret_cast<float4*>((float*)a.actw + off) = o;
                     if (u == a.top_u)
                         omax = fmaxf(omax, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
                 }
@@ -544,8 +552,20 @@ void launch_gram_fwd(const GramArgs& a, hipStream_t s) {
 void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gram_bwd_f, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
+static int gram_nt() {   // ASTYLE_GRAM_NT=1 / 2 / 3: nontemporal loads / stores / both (A/B; default 0)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("ASTYLE_GRAM_NT"); v = e ? (atoi(e) & 3) : 0; }
+    return v;
+}
 void launch_gram_bwd_s(const GramArgs& a, hipStream_t s) {
     const dim3 grid(a.B * a.nchunk * (C / GCS));
+    if (const int nt = gram_nt()) {
+#define NT_LAUNCH(M) { if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 2, M>), grid, dim3(GWT), 0, s, a); \
+                       else hipLaunchKernelGGL((k_gram_bwd_s<false, 2, M>), grid, dim3(GWT), 0, s, a); }
+        if (nt == 1) NT_LAUNCH(1) else if (nt == 2) NT_LAUNCH(2) else NT_LAUNCH(3)
+#undef NT_LAUNCH
+        return;
+    }
     if (gram_bwd_stages() == 3) {
         if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 3>), grid, dim3(GWT), 0, s, a);
         else hipLaunchKernelGGL((k_gram_bwd_s<false, 3>), grid, dim3(GWT), 0, s, a);
