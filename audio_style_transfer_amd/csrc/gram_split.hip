@@ -68,7 +68,8 @@ __device__ __forceinline__ void split8(const float4 (&v)[8], uint4& hi, uint4& l
 // rows t0 + 8 (w >> 2) + k (k = 0..7): one load instruction covers 8 whole lines.
 // NST stages of loads in flight (2: 128 KiB per workgroup; 3: 192 KiB, the registers of a
 // third stage fit beside the accumulators at the same two waves per SIMD)
-template <int NST>
+// NTL (A/B, ASTYLE_GRAM_NT bit 2): nontemporal staging loads
+template <int NST, bool NTL = false>
 __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
     __shared__ __attribute__((aligned(16))) u16 I[GCS * 32 * FRS];   // [c][u][hi t | lo t]
     int b, ch, c0;
@@ -92,7 +93,12 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
     const int tend = tbeg + tlen;
     auto load = [&](float4 (&v)[8], int t0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
+        for (int k = 0; k < 8; ++k) {
+            if (NTL) {
+                const f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + (size_t)(t0 + k) * rs));
+                v[k] = make_float4(q[0], q[1], q[2], q[3]);
+            } else v[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
+        }
     };
     auto stage = [&](float4 (&v)[8], int t0) {
         uint4 fh[4], fl[4];          // channel 4 sq + j: 8 consecutive rows, hi / lo
@@ -542,8 +548,10 @@ static int gram_stages() {   // ASTYLE_GRAM_STAGES=2 / 3 (A/B; default 3)
     if (v < 0) { const char* e = getenv("ASTYLE_GRAM_STAGES"); v = e ? atoi(e) : 3; if (v != 2) v = 3; }
     return v;
 }
+static int gram_nt();
 void launch_gram_fwd_s(const GramArgs& a, hipStream_t s) {
-    if (gram_stages() == 2) hipLaunchKernelGGL(k_gram_fwd_s<2>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+    if (gram_nt() & 4) hipLaunchKernelGGL((k_gram_fwd_s<3, true>), dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+    else if (gram_stages() == 2) hipLaunchKernelGGL(k_gram_fwd_s<2>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
     else hipLaunchKernelGGL(k_gram_fwd_s<3>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
 void launch_gram_fwd(const GramArgs& a, hipStream_t s) {
@@ -552,14 +560,14 @@ void launch_gram_fwd(const GramArgs& a, hipStream_t s) {
 void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gram_bwd_f, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
-static int gram_nt() {   // ASTYLE_GRAM_NT=1 / 2 / 3: nontemporal loads / stores / both (A/B; default 0)
+static int gram_nt() {   // ASTYLE_GRAM_NT bits: 1 / 2 backward nontemporal loads / stores, 4 forward loads (A/B; default 0)
     static int v = -1;
-    if (v < 0) { const char* e = getenv("ASTYLE_GRAM_NT"); v = e ? (atoi(e) & 3) : 0; }
+    if (v < 0) { const char* e = getenv("ASTYLE_GRAM_NT"); v = e ? (atoi(e) & 7) : 0; }
     return v;
 }
 void launch_gram_bwd_s(const GramArgs& a, hipStream_t s) {
     const dim3 grid(a.B * a.nchunk * (C / GCS));
-    if (const int nt = gram_nt()) {
+    if (const int nt = gram_nt() & 3) {
 #define NT_LAUNCH(M) { if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 2, M>), grid, dim3(GWT), 0, s, a); \
                        else hipLaunchKernelGGL((k_gram_bwd_s<false, 2, M>), grid, dim3(GWT), 0, s, a); }
         if (nt == 1) NT_LAUNCH(1) else if (nt == 2) NT_LAUNCH(2) else NT_LAUNCH(3)
