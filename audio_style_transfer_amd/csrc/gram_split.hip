@@ -68,8 +68,7 @@ __device__ __forceinline__ void split8(const float4 (&v)[8], uint4& hi, uint4& l
 // rows t0 + 8 (w >> 2) + k (k = 0..7): one load instruction covers 8 whole lines.
 // NST stages of loads in flight (2: 128 KiB per workgroup; 3: 192 KiB, the registers of a
 // third stage fit beside the accumulators at the same two waves per SIMD)
-// NTL (A/B, ASTYLE_GRAM_NT bit 2): nontemporal staging loads
-template <int NST, bool NTL = false>
+template <int NST>
 __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
     __shared__ __attribute__((aligned(16))) u16 I[GCS * 32 * FRS];   // [c][u][hi t | lo t]
     int b, ch, c0;
@@ -93,12 +92,7 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
     const int tend = tbeg + tlen;
     auto load = [&](float4 (&v)[8], int t0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (NTL) {
-                const f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + (size_t)(t0 + k) * rs));
-                v[k] = make_float4(q[0], q[1], q[2], q[3]);
-            } else v[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
-        }
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
     };
     auto stage = [&](float4 (&v)[8], int t0) {
         uint4 fh[4], fl[4];          // channel 4 sq + j: 8 consecutive rows, hi / lo
@@ -147,8 +141,7 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
 // CONT: the fused content tap (a.cont_u >= 0); false: the round-2 kernel.  NST stages of loads
 // in flight: 2 (the split of a stage into registers before the barrier) or 3 (each channel split
 // straight into the image after the barrier: 24 fewer live registers pay for the third stage)
-// NTM (A/B, ASTYLE_GRAM_NT): bit 0 nontemporal staging loads of E, bit 1 nontemporal D stores
-template <bool CONT, int NST, int NTM = 0>
+template <bool CONT, int NST>
 __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     __shared__ __attribute__((aligned(16))) u16 IH[GCS * GSS * BRS];       // [c][t][u] hi
     __shared__ __attribute__((aligned(16))) u16 IL[GCS * GSS * BRS];       // [c][t][u] lo
@@ -204,13 +197,7 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     float4 vr[NST][8];
     auto load = [&](float4 (&v)[8], int t0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float4* src = reinterpret_cast<const float4*>(ld[k] + (lrs[k] ? lofs + (uint32_t)(t0 + st) * C : 0u));
-            if (NTM & 1) {
-                const f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src));
-                v[k] = make_float4(q[0], q[1], q[2], q[3]);
-            } else v[k] = *src;
-        }
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (lrs[k] ? lofs + (uint32_t)(t0 + st) * C : 0u));
     };
     auto stage = [&](float4 (&v)[8], int t0) {
         float4 ce, cph = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -299,8 +286,7 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
                         o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
                     }
                     if (CONT && u == a.cont_u) { o.x += cadd.x; o.y += cadd.y; o.z += cadd.z; o.w += cadd.w; }
-                    if (NTM & 2) __builtin_nontemporal_store(f32x4{o.x, o.y, o.z, o.w}, reinterpret_cast<f32x4*>((float*)a.actw + off));
-                    else *reinterpret_cast<float4*>((float*)a.actw + off) = o;
+                    *reinterpret_cast<float4*>((float*)a.actw + off) = o;
                     if (u == a.top_u)
                         omax = fmaxf(omax, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
                 }
@@ -548,10 +534,8 @@ static int gram_stages() {   // ASTYLE_GRAM_STAGES=2 / 3 (A/B; default 3)
     if (v < 0) { const char* e = getenv("ASTYLE_GRAM_STAGES"); v = e ? atoi(e) : 3; if (v != 2) v = 3; }
     return v;
 }
-static int gram_nt();
 void launch_gram_fwd_s(const GramArgs& a, hipStream_t s) {
-    if (gram_nt() & 4) hipLaunchKernelGGL((k_gram_fwd_s<3, true>), dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
-    else if (gram_stages() == 2) hipLaunchKernelGGL(k_gram_fwd_s<2>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+    if (gram_stages() == 2) hipLaunchKernelGGL(k_gram_fwd_s<2>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
     else hipLaunchKernelGGL(k_gram_fwd_s<3>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
 void launch_gram_fwd(const GramArgs& a, hipStream_t s) {
@@ -560,20 +544,8 @@ void launch_gram_fwd(const GramArgs& a, hipStream_t s) {
 void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gram_bwd_f, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
-static int gram_nt() {   // ASTYLE_GRAM_NT bits: 1 / 2 backward nontemporal loads / stores, 4 forward loads (A/B; default 0)
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("ASTYLE_GRAM_NT"); v = e ? (atoi(e) & 7) : 0; }
-    return v;
-}
 void launch_gram_bwd_s(const GramArgs& a, hipStream_t s) {
     const dim3 grid(a.B * a.nchunk * (C / GCS));
-    if (const int nt = gram_nt() & 3) {
-#define NT_LAUNCH(M) { if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 2, M>), grid, dim3(GWT), 0, s, a); \
-                       else hipLaunchKernelGGL((k_gram_bwd_s<false, 2, M>), grid, dim3(GWT), 0, s, a); }
-        if (nt == 1) NT_LAUNCH(1) else if (nt == 2) NT_LAUNCH(2) else NT_LAUNCH(3)
-#undef NT_LAUNCH
-        return;
-    }
     if (gram_bwd_stages() == 3) {
         if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 3>), grid, dim3(GWT), 0, s, a);
         else hipLaunchKernelGGL((k_gram_bwd_s<false, 3>), grid, dim3(GWT), 0, s, a);
