@@ -105,6 +105,7 @@ struct ast_ctx {
     std::vector<Occ> occ;
     int ncc = 0;
     int nchunk = 1;
+    int nchunk_b = 1;     // split ours-Gram backward: its own time chunks (see plan())
     void* cg_buf[NBLK_MAX + 1] = {};        // content grad per tensor (or null), storage type
     bool tensor_in_style[NBLK_MAX + 1] = {};
     bool tensor_has_direct_content[NBLK_MAX + 1] = {};
@@ -224,6 +225,23 @@ int plan(const ast_cfg* c, ast_ctx* x) {
         x->smat_elems = (size_t)c->batch * C * 1024;
     }
     x->nchunk = nch;
+    // The split ours-Gram backward (D = S~ E, row-independent) may cut time finer than the
+    // forward, whose per-chunk Gram partials fix the summation order: at few clips the
+    // forward's chunks leave most CUs idle (one clip: 16 workgroups).  Its only cross-row sums,
+    // the fused content tap's squared errors, go to fixed GRAM_CSLOT-row slots, so every
+    // result stays independent of the batch.  Chunks: the fewest whole-slot chunks, at least
+    // the forward's count, that give >= 1024 workgroups.
+    x->nchunk_b = nch;
+    if (c->precision == 2 && !c->gatys) {
+        const int slots = c->T / GRAM_CSLOT;
+        int d = 1;
+        for (int k = 1; k <= slots; ++k) {
+            if (slots % k) continue;
+            d = k;
+            if (k >= nch && (size_t)c->batch * k * 4 >= 1024) break;
+        }
+        x->nchunk_b = d;
+    }
     return 0;
 }
 
@@ -901,7 +919,7 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
     for (int t = 0; t <= NBLK_MAX; ++t) first_cg[t] = true;
     bool first_bott = true;
     const int fuse_u = fused_content_occ(x);
-    if (fuse_u >= 0)   // the Gram backward writes nchunk x 4 of the occurrence's partial slots per clip
+    if (fuse_u >= 0)   // the Gram backward writes (T / GRAM_CSLOT) x 4 = ncpart partial slots per clip
         launch_zero32(x->cpart, (size_t)c.batch * x->ncpart * 4, s);
     for (size_t i = 0; i < x->occ.size(); ++i) {
         if (fuse_u >= 0) break;
@@ -963,6 +981,7 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
             g.cont_ncc = x->ncc; g.cont_off = o.off; g.cont_ncol = o.ncol; g.cont_coef = ccoef;
             g.cont_part = x->cpart; g.cont_pstride = (size_t)x->ncpart;
         }
+        g.nchunk = x->nchunk_b;
         launch_gram_bwd_any(x, g, s);
     }
     tmark(x, s);

@@ -243,7 +243,7 @@ struct GramArgs {
     unsigned* gmax_top;                     // ... goes to gmax_top[b] (atomic max of float bits), or -1
     // split bwd, fused content tap (methods.py:116-117): for unique tensor cont_u (or -1) D +=
     // coef (E - phi[..., off + c]) on channels c < ncol, in place of k_content's cg buffer round
-    // trip; the workgroup's sum of squared errors goes to cont_part[b * cont_pstride + chunk *
+    // trip; the squared errors of every GRAM_CSLOT rows of a workgroup go to cont_part[b * cont_pstride + slot *
     // (C / 32) + channel group]
     int cont_u;
     const float* cont_phi; size_t cont_phi_bstride;
@@ -333,6 +333,8 @@ void launch_style_gatys(const GatysStyleArgs& a, hipStream_t s);
 constexpr int GY_ROWS = 512;    // Gatys bwd: time rows per workgroup
 void launch_content(const ContentArgs& a, hipStream_t s);
 constexpr int CROWS = 64;   // rows per content workgroup
+constexpr int GRAM_CSLOT = 256;   // rows per content-error slot of the fused split Gram backward
+static_assert((512 / GRAM_CSLOT) * 4 == 512 / CROWS, "fused content slots fill ncpart of one occurrence");
 void launch_finalize(float* parts, const float* cpart, int ncpart, float cscale,
                      const float* spart, int nspart, float sscale, float lambd, int B,
                      hipStream_t s);

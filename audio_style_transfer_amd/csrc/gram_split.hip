@@ -20,6 +20,7 @@
 // Loads and stores move whole 128-B lines (8 lanes x 16 B per row).
 #include "common.h"
 #include <cstdlib>
+#include <cstdio>
 
 namespace ast {
 namespace {
@@ -152,7 +153,8 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     float omax = 0.f;   // max |D| of tensor top_u (the backward chain's first input: no k_absmax pass)
-    float csd = 0.f;    // squared content error of tensor cont_u
+    float csd = 0.f;    // squared content error of tensor cont_u (this GRAM_CSLOT-row slot)
+    __shared__ float cws[GWT / 64];
     const int i16 = lane & 15, kq = lane >> 4;
     // A fragments (16x16x32): S~_c[u = 16 m + i16][u' = 8 kq .. + 8] as bf16 hi / lo; wave w
     // owns channels 4 w .. 4 w + 3
@@ -296,10 +298,28 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
 #pragma unroll
     for (int q = 0; q < NST; ++q)
         if (tbeg + q * GSS < tend) load(vr[q], tbeg + q * GSS);
+    // the content errors of every GRAM_CSLOT rows -> their own slot (fixed order: wave butterfly,
+    // then waves 0..7), so the loss does not depend on how time is cut into workgroups
+    auto flush_c = [&](int slot) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) csd += __shfl_xor(csd, off);
+        if (lane == 0) cws[w] = csd;
+        __syncthreads();
+        if (tid == 0) {
+            float v = 0.f;
+#pragma unroll
+            for (int k = 0; k < GWT / 64; ++k) v += cws[k];
+            a.cont_part[(size_t)b * a.cont_pstride + slot * (C / GCS) + c0 / GCS] = v;
+        }
+        csd = 0.f;
+    };
     for (int t0 = tbeg; t0 < tend; t0 += NST * GSS) {
 #pragma unroll
         for (int q = 0; q < NST; ++q)
-            if (t0 + q * GSS < tend) stage(vr[q], t0 + q * GSS);
+            if (t0 + q * GSS < tend) {
+                stage(vr[q], t0 + q * GSS);
+                if (CONT && (t0 + (q + 1) * GSS) % GRAM_CSLOT == 0) flush_c((t0 + q * GSS) / GRAM_CSLOT);
+            }
     }
     if (a.top_u >= 0) {   // one atomic per workgroup
         __shared__ float wm[GWT / 64];
@@ -312,19 +332,6 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
 #pragma unroll
             for (int k = 1; k < GWT / 64; ++k) m = fmaxf(m, wm[k]);
             atomicMax(a.gmax_top + b, __float_as_uint(m));
-        }
-    }
-    if (CONT) {           // the workgroup's content partial (a plain store: one slot per workgroup)
-        __shared__ float ws[GWT / 64];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) csd += __shfl_xor(csd, off);
-        if (lane == 0) ws[w] = csd;
-        __syncthreads();
-        if (tid == 0) {
-            float v = 0.f;
-#pragma unroll
-            for (int k = 0; k < GWT / 64; ++k) v += ws[k];
-            a.cont_part[(size_t)b * a.cont_pstride + ch * (C / GCS) + c0 / GCS] = v;
         }
     }
 }
@@ -546,6 +553,10 @@ void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
 }
 void launch_gram_bwd_s(const GramArgs& a, hipStream_t s) {
     const dim3 grid(a.B * a.nchunk * (C / GCS));
+    if (a.cont_u >= 0 && (a.T / a.nchunk) % GRAM_CSLOT) {
+        fprintf(stderr, "gram_bwd_s: the fused content tap needs whole %d-row chunks\n", GRAM_CSLOT);
+        abort();
+    }
     if (gram_bwd_stages() == 3) {
         if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 3>), grid, dim3(GWT), 0, s, a);
         else hipLaunchKernelGGL((k_gram_bwd_s<false, 3>), grid, dim3(GWT), 0, s, a);
