@@ -136,6 +136,76 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
     }
 }
 
+// forward for few clips (k_gram_fwd_n): 8 channels per workgroup instead of 32, so a clip's
+// chunk spreads over 16 workgroups instead of 4 (one clip: 64 instead of 16).  Wave w owns
+// channel c0 + w and runs, stage by stage (16 rows), the same three MFMAs on the same
+// fragments as k_gram_fwd_s's wave for that channel: the partials are bit-identical, so a
+// clip's result does not depend on which kernel the batch size selects.  Staging: a fill is 4
+// stages (64 rows); thread (w, l) loads tensor 8 (w & 3) + (l & 7), channel quad (l >> 3) & 1,
+// rows 8 g .. + 8 of the fill, g = (l >> 4) + 4 (w >> 2); two fills of loads in flight.
+constexpr int GCN = 8;        // channels per narrow forward workgroup
+constexpr int GFN = 64;       // rows per narrow fill (4 stages)
+__global__ void __launch_bounds__(GWT) k_gram_fwd_n(GramArgs a) {
+    __shared__ __attribute__((aligned(16))) u16 I[(GFN / GSS) * GCN * 32 * FRS];   // [stage][c][u][hi | lo]
+    constexpr int ncg = C / GCN;
+    const int nwg = a.B * a.nchunk * ncg;
+    int work = xcd_remap(blockIdx.x, nwg);
+    const int cgi = work % ncg; work /= ncg;
+    const int ch = work % a.nchunk, b = work / a.nchunk, c0 = cgi * GCN;
+    const int tlen = a.T / a.nchunk, tbeg = ch * tlen, tend = tbeg + tlen;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int su = 8 * (w & 3) + (lane & 7), sq = (lane >> 3) & 1, g = (lane >> 4) + 4 * (w >> 2);
+    const bool real = su < a.nu;
+    const float* src = real ? (const float*)a.act + (size_t)a.uid[su] * a.tstride +
+                              (size_t)b * a.T * C + c0 + 4 * sq + (size_t)8 * g * C
+                            : (const float*)a.zero16;
+    const size_t rs = real ? C : 0;
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    float4 v[2][8];
+    auto load = [&](float4 (&vv)[8], int t0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) vv[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
+    };
+    auto fill = [&](float4 (&vv)[8], int t0) {
+        uint4 fh[4], fl[4];
+        split8<0>(vv, fh[0], fl[0]);
+        split8<1>(vv, fh[1], fl[1]);
+        split8<2>(vv, fh[2], fl[2]);
+        split8<3>(vv, fh[3], fl[3]);
+        if (t0 + 2 * GFN < tend) load(vv, t0 + 2 * GFN);
+        __syncthreads();   // the previous fill's MFMA reads are done
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            // stage g >> 1, channel 4 sq + j, tensor su; rows 8 (g & 1) .. of the stage
+            u16* row = &I[(((g >> 1) * GCN + 4 * sq + j) * 32 + su) * FRS + 8 * (g & 1)];
+            *reinterpret_cast<uint4*>(row) = fh[j];
+            *reinterpret_cast<uint4*>(row + 16) = fl[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int st = 0; st < GFN / GSS; ++st) {
+            const u16* row = &I[((st * GCN + w) * 32 + r) * FRS + 8 * h];
+            const uint4 xh = *reinterpret_cast<const uint4*>(row);
+            const uint4 xl = *reinterpret_cast<const uint4*>(row + 16);
+            acc = mfma_bf16(xh, xh, acc);
+            acc = mfma_bf16(xh, xl, acc);
+            acc = mfma_bf16(xl, xh, acc);
+        }
+    };
+    load(v[0], tbeg);
+    if (tbeg + GFN < tend) load(v[1], tbeg + GFN);
+    for (int t0 = tbeg; t0 < tend; t0 += 2 * GFN) {
+        fill(v[0], t0);
+        if (t0 + GFN < tend) fill(v[1], t0 + GFN);
+    }
+    float* dst = a.gpart + (((size_t)b * a.nchunk + ch) * C + c0 + w) * 1024;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dst[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = acc[i];
+}
+
 // backward.  Staging: thread (w, l) loads tensors 8 (w & 3) + k (k = 0..7), channel quad
 // l >> 3, row t0 + 8 (w >> 2) + (l & 7).  Output: 16 tensors at a time through O; padding
 // tensors (u >= nu) are neither read nor written.
@@ -542,6 +612,11 @@ static int gram_stages() {   // ASTYLE_GRAM_STAGES=2 / 3 (A/B; default 3)
     return v;
 }
 void launch_gram_fwd_s(const GramArgs& a, hipStream_t s) {
+    // few clips (under 2 workgroups per CU with 32-channel groups): the 8-channel kernel, same bits
+    if ((size_t)a.B * a.nchunk * (C / GCS) < 512 && (a.T / a.nchunk) % GFN == 0) {
+        hipLaunchKernelGGL(k_gram_fwd_n, dim3(a.B * a.nchunk * (C / GCN)), dim3(GWT), 0, s, a);
+        return;
+    }
     if (gram_stages() == 2) hipLaunchKernelGGL(k_gram_fwd_s<2>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
     else hipLaunchKernelGGL(k_gram_fwd_s<3>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
