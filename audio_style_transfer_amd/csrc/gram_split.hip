@@ -612,8 +612,10 @@ static int gram_stages() {   // ASTYLE_GRAM_STAGES=2 / 3 (A/B; default 3)
     return v;
 }
 void launch_gram_fwd_s(const GramArgs& a, hipStream_t s) {
-    // few clips (under 2 workgroups per CU with 32-channel groups): the 8-channel kernel, same bits
-    if ((size_t)a.B * a.nchunk * (C / GCS) < 512 && (a.T / a.nchunk) % GFN == 0) {
+    // very few clips (under 64 workgroups with 32-channel groups; measured: one clip 0.54 ->
+    // 0.28 ms, 8 clips 0.65 -> 0.78 ms, the 32-B row pieces cost more than the extra
+    // workgroups return): the 8-channel kernel, same bits
+    if ((size_t)a.B * a.nchunk * (C / GCS) < 64 && (a.T / a.nchunk) % GFN == 0) {
         hipLaunchKernelGGL(k_gram_fwd_n, dim3(a.B * a.nchunk * (C / GCN)), dim3(GWT), 0, s, a);
         return;
     }
