@@ -3,7 +3,7 @@ bands (api.hip dalloc); the caller's buffers (x, grad, parts, targets) are slice
 tensors whose margins hold a sentinel.  Runs embeds, eager loss_grad and a captured graph's
 replays for a few configurations and reports every band that was written.
 
-  ASTYLE_GUARD=1 python tools/guard_check.py"""
+  ASTYLE_GUARD=1 python tools/guard_check.py [--quick]"""
 import ctypes
 import os
 import sys
@@ -86,9 +86,13 @@ def main():
     assert os.environ.get('ASTYLE_GUARD') == '1', 'run with ASTYLE_GUARD=1'
     dev = torch.device('cuda', 0)
     bad = False
-    for B, T, gatys, prec in ((8, 16384, False, 'split'), (3, 16384, False, 'split'),
-                              (8, 16384, True, 'split'), (2, 4096, False, 'split'),
-                              (4, 16384, False, 'fp32'), (4, 16384, False, 'bf16')):
+    cases = ((8, 16384, False, 'split'), (3, 16384, False, 'split'), (1, 16384, False, 'split'),
+             (8, 16384, True, 'split'), (2, 4096, False, 'split'),
+             (4, 16384, False, 'fp32'), (4, 16384, False, 'bf16'))
+    if '--quick' in sys.argv:   # (tests/test_gpu_guard.py)
+        cases = ((1, 16384, False, 'split'), (3, 4096, False, 'split'), (2, 4096, True, 'split'),
+                 (2, 2048, False, 'fp32'), (2, 2048, False, 'bf16'))
+    for B, T, gatys, prec in cases:
         bad |= case(B, T, gatys, prec, dev)
     print('OUT-OF-BOUNDS STORES FOUND' if bad else 'no out-of-bounds stores', flush=True)
 
