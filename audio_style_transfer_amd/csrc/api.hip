@@ -225,14 +225,14 @@ int plan(const ast_cfg* c, ast_ctx* x) {
         x->smat_elems = (size_t)c->batch * C * 1024;
     }
     x->nchunk = nch;
-    // The split ours-Gram backward (D = S~ E, row-independent) may cut time finer than the
+    // The split / fp32 ours-Gram backward (D = S~ E, row-independent) may cut time finer than the
     // forward, whose per-chunk Gram partials fix the summation order: at few clips the
     // forward's chunks leave most CUs idle (one clip: 16 workgroups).  Its only cross-row sums,
     // the fused content tap's squared errors, go to fixed GRAM_CSLOT-row slots, so every
     // result stays independent of the batch.  Chunks: the fewest whole-slot chunks, at least
     // the forward's count, that give >= 1024 workgroups.
     x->nchunk_b = nch;
-    if (c->precision == 2 && !c->gatys) {
+    if ((c->precision == 2 || c->precision == 0) && !c->gatys) {   // (fp32's k_gram_bwd_f: no cross-row sums)
         const int slots = c->T / GRAM_CSLOT;
         int d = 1;
         for (int k = 1; k <= slots; ++k) {
