@@ -488,6 +488,81 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_f(GramArgs a) {
     }
 }
 
+// fp32 forward for very few clips: k_gram_fwd_n's staging (8 channels, 64-row fills, wave w
+// = channel c0 + w) with k_gram_fwd_f's per-channel MFMA sequence, stage by stage: the same
+// partials bit for bit
+__global__ void __launch_bounds__(GWT) k_gram_fwd_fn(GramArgs a) {
+    __shared__ __attribute__((aligned(16))) float I[(GFN / GSS) * GCN * 32 * FRF];   // [stage][c][u][t]
+    constexpr int ncg = C / GCN;
+    const int nwg = a.B * a.nchunk * ncg;
+    int work = xcd_remap(blockIdx.x, nwg);
+    const int cgi = work % ncg; work /= ncg;
+    const int ch = work % a.nchunk, b = work / a.nchunk, c0 = cgi * GCN;
+    const int tlen = a.T / a.nchunk, tbeg = ch * tlen, tend = tbeg + tlen;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int i16 = lane & 15, kq = lane >> 4;
+    const int su = 8 * (w & 3) + (lane & 7), sq = (lane >> 3) & 1, g = (lane >> 4) + 4 * (w >> 2);
+    const bool real = su < a.nu;
+    const float* src = real ? (const float*)a.act + (size_t)a.uid[su] * a.tstride +
+                              (size_t)b * a.T * C + c0 + 4 * sq + (size_t)8 * g * C
+                            : (const float*)a.zero16;
+    const size_t rs = real ? C : 0;
+    f32x4 acc[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 v[2][8];
+    auto load = [&](float4 (&vv)[8], int t0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) vv[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
+    };
+    auto fill = [&](float4 (&vv)[8], int t0) {
+        float4 f[4][2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            auto e = [&](int k) { return j == 0 ? vv[k].x : j == 1 ? vv[k].y : j == 2 ? vv[k].z : vv[k].w; };
+            f[j][0] = make_float4(e(0), e(1), e(2), e(3));
+            f[j][1] = make_float4(e(4), e(5), e(6), e(7));
+        }
+        if (t0 + 2 * GFN < tend) load(vv, t0 + 2 * GFN);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float* row = &I[(((g >> 1) * GCN + 4 * sq + j) * 32 + su) * FRF + 8 * (g & 1)];
+            *reinterpret_cast<float4*>(row) = f[j][0];
+            *reinterpret_cast<float4*>(row + 4) = f[j][1];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int sg = 0; sg < GFN / GSS; ++sg) {
+            const float* base = &I[(sg * GCN + w) * 32 * FRF + 4 * kq];
+            const float4 u0 = *reinterpret_cast<const float4*>(base + i16 * FRF);
+            const float4 u1 = *reinterpret_cast<const float4*>(base + (16 + i16) * FRF);
+            const float a0[4] = {u0.x, u0.y, u0.z, u0.w}, a1[4] = {u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[st], a0[st], acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[st], a1[st], acc[1], 0, 0, 0);
+                acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[st], a1[st], acc[2], 0, 0, 0);
+            }
+        }
+    };
+    load(v[0], tbeg);
+    if (tbeg + GFN < tend) load(v[1], tbeg + GFN);
+    for (int t0 = tbeg; t0 < tend; t0 += 2 * GFN) {
+        fill(v[0], t0);
+        if (t0 + GFN < tend) fill(v[1], t0 + GFN);
+    }
+    float* dst = a.gpart + (((size_t)b * a.nchunk + ch) * C + c0 + w) * 1024;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int rr = 4 * kq + i;
+        dst[rr * 32 + i16] = acc[0][i];
+        dst[rr * 32 + 16 + i16] = acc[1][i];
+        dst[(16 + i16) * 32 + rr] = acc[1][i];
+        dst[(16 + rr) * 32 + 16 + i16] = acc[2][i];
+    }
+}
+
 // backward: image [c][t][u] fp32, 32 floats per row with the four 8-tensor blocks swizzled
 // (block kq of row t at 8 (kq ^ (t & 3)): conflict-free 16-B reads); D_c = S~_c E_c on
 // v_mfma_f32_16x16x4f32: A = S~_c[u = 16 m + i16][u' = 8 kq + ks] in registers, B: lane
@@ -623,6 +698,10 @@ void launch_gram_fwd_s(const GramArgs& a, hipStream_t s) {
     else hipLaunchKernelGGL(k_gram_fwd_s<3>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
 void launch_gram_fwd(const GramArgs& a, hipStream_t s) {
+    if ((size_t)a.B * a.nchunk * (C / GCS) < 64 && (a.T / a.nchunk) % GFN == 0) {   // (as launch_gram_fwd_s)
+        hipLaunchKernelGGL(k_gram_fwd_fn, dim3(a.B * a.nchunk * (C / GCN)), dim3(GWT), 0, s, a);
+        return;
+    }
     hipLaunchKernelGGL(k_gram_fwd_f, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
 void launch_gram_bwd(const GramArgs& a, hipStream_t s) {

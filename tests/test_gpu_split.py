@@ -253,6 +253,28 @@ def test_split_graph_replay_matches_eager(weights, dev):
     assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
 
 
+@pytest.mark.parametrize('precision', ['split', 'fp32'])
+def test_few_clip_gram_kernels_bit_identical(precision, dev):
+    """At one clip the ours-Gram runs the 8-channel forward (k_gram_fwd_n / k_gram_fwd_fn) and a
+    64-chunk backward; at 16 clips the 32-channel kernels and 4 chunks: the same clip gives the
+    same loss parts and gradient bit for bit (the ours-Gram at few clips)."""
+    import bench
+    from audio_style_transfer_amd.engine import StyleEngine
+    T, B = 16384, 16
+    e16 = StyleEngine(B, T, [29], list(range(30)), precision=precision, device=dev, lambd=100.0)
+    x16 = bench.make_problem(e16, list(range(B)), T, dev)
+    p16, g16 = e16.loss_grad(x16)
+    phi_c, phi_s = e16._targets
+    k = 11
+    e1 = StyleEngine(1, T, [29], list(range(30)), precision=precision, device=dev, lambd=100.0)
+    e1.set_targets(phi_c[k:k + 1].clone(), phi_s[k:k + 1].clone())
+    p1, g1 = e1.loss_grad(x16[k:k + 1].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(p1[0], p16[k]) and torch.equal(g1[0], g16[k])
+    e16.close()
+    e1.close()
+
+
 def test_graph_replays_bitwise_at_bench_length(dev):
     """Every replay of a captured ast_loss_grad equals the eager call bit for bit, at the bench's
     clip length with 8 clips (one per XCD in the block kernels' tile order), with eager work
