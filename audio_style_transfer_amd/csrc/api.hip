@@ -269,6 +269,13 @@ static bool d_out_of_place() {
     if (v < 0) { const char* e = getenv("ASTYLE_DOOP"); v = e ? (atoi(e) != 0) : 1; }
     return v != 0;
 }
+// Byte offset of the D buffer inside its allocation (ASTYLE_DPAD, A/B of the Gram backward's
+// read / write address interplay; a multiple of 256)
+static size_t d_pad() {
+    static long v = -1;
+    if (v < 0) { const char* e = getenv("ASTYLE_DPAD"); v = e ? (std::max(0L, atol(e)) / 256) * 256 : 0; }
+    return (size_t)v;
+}
 
 int fused_content_occ(const ast_ctx* x);
 
@@ -279,6 +286,7 @@ size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     n += W_TOTAL * 4 + (size_t)NBLK_MAX * BLKB_SZ * 2;
     if (c->precision == 2) n += (size_t)NBLK_MAX * SBLK * 16 + 2 * (size_t)(NBLK_MAX + 1) * c->batch * 4;
     n += (size_t)(x->nblk + 1) * (BTC + tensor_pad()) * es * (d_out_of_place() ? 2 : 1);   // act (+ D)
+    if (d_out_of_place()) n += d_pad();
     n += 2 * (size_t)x->nblk * c->batch * c->T * 16;        // mu, me
     n += 2 * BTC * es;                                      // chain
     int ncg = 0;
@@ -640,7 +648,10 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     ALLOC(x->wtsb, (size_t)NBLK_MAX * BLKB_SZ * 2);
     (void)hipMemset(x->wtsb, 0, (size_t)NBLK_MAX * BLKB_SZ * 2);
     ALLOC(x->act, (size_t)(x->nblk + 1) * x->tstride * x->esz);
-    if (d_out_of_place()) ALLOC(x->dgrad, (size_t)(x->nblk + 1) * x->tstride * x->esz);
+    if (d_out_of_place()) {
+        ALLOC(x->dgrad, (size_t)(x->nblk + 1) * x->tstride * x->esz + d_pad());
+        x->dgrad = (char*)x->dgrad + d_pad();   // (x->allocs keeps the base for hipFree)
+    }
     ALLOC(x->mu, (size_t)x->nblk * c.batch * c.T * 16);
     ALLOC(x->me, (size_t)x->nblk * c.batch * c.T * 16);
     ALLOC(x->chain[0], BTC * x->esz);
