@@ -121,7 +121,7 @@ struct ast_ctx {
     unsigned* gmax_g = nullptr;             // [nblk + 1][B] max |d loss / d e_l| per clip
     size_t esz = 4;                         // bytes per stored element
     void* act = nullptr; size_t tstride = 0;
-    void* dgrad = nullptr;   // style-tapped tensors' D out of place (default; ASTYLE_DOOP=0: in place over act)
+    void* dgrad = nullptr;   // style-tapped tensors' D out of place (ASTYLE_DOOP=1; default: in place over act)
     uint32_t* mu = nullptr; uint32_t* me = nullptr;
     void* chain[2] = {};
     float* bott = nullptr; float* gbott = nullptr;
@@ -260,13 +260,14 @@ static size_t tensor_pad() {
     return (size_t)pad;
 }
 
-// The Gram backward writes D (the direct loss gradients of the style-tapped tensors) to a buffer of
-// its own instead of over E: +1 activation set of memory, and the kernel no longer switches
-// between ~23 and ~27 ms per process (measured 24.2 ms every time out of place, B = 256,
-// T = 16384).  ASTYLE_DOOP=0 restores the in-place layout (larger batches per GPU).
+// Where the Gram backward writes D (the direct loss gradients of the style-tapped tensors): over E
+// in place (default since round 4: 24.14-24.18 ms in 5 of 5 processes against 25.0-25.1 out of
+// place, B = 256, T = 16384, with the tensor pad and the round-4 kernels; round 2 had measured
+// in place switching between ~23 and ~27 ms per process before the pad), or, ASTYLE_DOOP=1, to a
+// buffer of its own (+1 activation set of memory).
 static bool d_out_of_place() {
     static int v = -1;
-    if (v < 0) { const char* e = getenv("ASTYLE_DOOP"); v = e ? (atoi(e) != 0) : 1; }
+    if (v < 0) { const char* e = getenv("ASTYLE_DOOP"); v = e ? (atoi(e) != 0) : 0; }
     return v != 0;
 }
 // Byte offset of the D buffer inside its allocation (ASTYLE_DPAD, A/B of the Gram backward's
