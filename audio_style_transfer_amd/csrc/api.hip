@@ -418,14 +418,15 @@ void launch_gram_bwd_any(ast_ctx* x, const GramArgs& g, hipStream_t s) {
     else launch_gram_bwd(g, s);
 }
 
-// The split ours-Gram backward computes the content tap's gradient and squared error itself
-// when there is exactly one content occurrence and its tensor is style-tapped (configs[2]:
-// cont 29): k_content's cg buffer (written, then read back by the Gram backward) is skipped.
+// The split Gram backward (ours or Gatys) computes the content tap's gradient and squared error
+// itself when there is exactly one content occurrence and its tensor is style-tapped (configs[2]
+// and configs[4]: cont 29): k_content's cg buffer (written, then read back by the Gram backward)
+// is skipped.
 // ASTYLE_FUSE_CONTENT=0 keeps the separate kernel.
 int fused_content_occ(const ast_ctx* x) {
     static int en = -1;
     if (en < 0) { const char* e = getenv("ASTYLE_FUSE_CONTENT"); en = e ? (atoi(e) != 0) : 1; }
-    if (!en || x->cfg.precision != 2 || x->cfg.gatys || x->occ.size() != 1 || x->need_bott) return -1;
+    if (!en || x->cfg.precision != 2 || x->occ.size() != 1 || x->need_bott) return -1;
     const Occ& o = x->occ[0];
     if (o.ext == 31 || !x->tensor_in_style[o.tensor]) return -1;
     if (o.off % 4 || o.ncol % 4 || x->ncc % 4) return -1;   // (float4 phi reads)
@@ -470,6 +471,7 @@ GatysArgs gatys_args(ast_ctx* x) {
     for (int u = 0; u < x->nu; ++u) { g.uid[u] = x->uid[u]; g.cg[u] = x->cg_buf[x->uid[u]]; }
     g.gpart = x->gpart; g.smat = x->smat; g.smatb = x->smatb;
     g.B = x->cfg.batch; g.T = x->cfg.T; g.nchunk = x->nchunk;
+    g.cont_u = -1;
     return g;
 }
 
@@ -968,6 +970,14 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
         sa.smat = x->smat; sa.smatb = x->smatb; sa.spart = x->spart;
         launch_style_gatys(sa, s);
         tmark(x, s);
+        if (fuse_u >= 0) {   // the split Gatys backward adds the content tap (one slot per 512-row tile)
+            const Occ& o = x->occ[0];
+            g.cg[fuse_u] = nullptr;
+            g.cont_u = fuse_u;
+            g.cont_phi = x->phi_c; g.cont_phi_bstride = x->phi_c_shared ? 0 : (size_t)c.T * x->ncc;
+            g.cont_ncc = x->ncc; g.cont_off = o.off; g.cont_ncol = o.ncol; g.cont_coef = ccoef;
+            g.cont_part = x->cpart; g.cont_pstride = (size_t)x->ncpart;
+        }
         launch_gatys_bwd(g, x->split ? 2 : (x->bf ? 1 : 0), s);
     } else {
         GramArgs g = gram_args(x);

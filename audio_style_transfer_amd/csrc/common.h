@@ -272,6 +272,13 @@ struct GatysArgs {
     const float* smat;                      // [B][nu][C][C]  S~ = sum_l dG_l + dG_l^T (fp32)
     const u16* smatb;                       // same, bf16 (precision 1)
     int B, T, nchunk;
+    // split bwd, fused content tap (as GramArgs): tensor cont_u (or -1) gets coef (E - phi) on its
+    // channels < cont_ncol; each workgroup's squared error goes to cont_part[b * cont_pstride + tile]
+    int cont_u;
+    const float* cont_phi; size_t cont_phi_bstride;
+    int cont_ncc, cont_off, cont_ncol;
+    float cont_coef;
+    float* cont_part; size_t cont_pstride;
 };
 
 struct GatysStyleArgs {
@@ -333,6 +340,7 @@ void launch_style_gatys(const GatysStyleArgs& a, hipStream_t s);
 constexpr int GY_ROWS = 512;    // Gatys bwd: time rows per workgroup
 void launch_content(const ContentArgs& a, hipStream_t s);
 constexpr int CROWS = 64;   // rows per content workgroup
+static_assert(GY_ROWS >= CROWS, "the fused Gatys content tap's T / GY_ROWS slots fit ncpart = T / CROWS");
 constexpr int GRAM_CSLOT = 256;   // rows per content-error slot of the fused split Gram backward
 static_assert((512 / GRAM_CSLOT) * 4 == 512 / CROWS, "fused content slots fill ncpart of one occurrence");
 void launch_finalize(float* parts, const float* cpart, int ncpart, float cscale,

@@ -415,99 +415,17 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
     }
 }
 
-__global__ void __launch_bounds__(256) k_gatys_bwd_s(GatysArgs a) {
-    __shared__ __attribute__((aligned(16))) u16 Sh[C * SBS];   // S~ hi
-    __shared__ __attribute__((aligned(16))) u16 Sl[C * SBS];   // S~ lo
-    const int tilesPer = a.T / GY_ROWS;
-    int bid = blockIdx.x;
-    const int tile = bid % tilesPer; bid /= tilesPer;
-    const int u = bid % a.nu, b = bid / a.nu;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const float* S = a.smat + ((size_t)b * a.nu + u) * (C * C);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int i = tid + 256 * k, row = i >> 4, c8 = i & 15;   // 8 values per piece
-        const float4 x0 = *reinterpret_cast<const float4*>(S + row * C + c8 * 8);
-        const float4 x1 = *reinterpret_cast<const float4*>(S + row * C + c8 * 8 + 4);
-        uint32_t h[4], l[4];
-        split2g(x0.x, x0.y, h[0], l[0]);
-        split2g(x0.z, x0.w, h[1], l[1]);
-        split2g(x1.x, x1.y, h[2], l[2]);
-        split2g(x1.z, x1.w, h[3], l[3]);
-        *reinterpret_cast<uint4*>(&Sh[row * SBS + c8 * 8]) = make_uint4(h[0], h[1], h[2], h[3]);
-        *reinterpret_cast<uint4*>(&Sl[row * SBS + c8 * 8]) = make_uint4(l[0], l[1], l[2], l[3]);
-    }
-    const float* E = (const float*)a.act + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;
-    float* Ew = (float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;   // D (in place unless out of place)
-    const float* CG = (const float*)a.cg[u];
-    if (CG) CG += (size_t)b * a.T * C;
-    const int j = lane & 31, kg = lane >> 5;
-    const int rows_w = GY_ROWS / 4;
-    const int t0 = tile * GY_ROWS + w * rows_w;
-    // lane (j, kg): time row t + j, channels kg 64 .. + 63 as 8 k-steps of 8
-    float4 cur[16], nxt[16];
-    auto loadB = [&](int t, float4 (&bb)[16]) {
-        const float4* src = reinterpret_cast<const float4*>(E + (size_t)(t + j) * C + kg * 64);
-#pragma unroll
-        for (int s = 0; s < 16; ++s) bb[s] = src[s];
-    };
-    loadB(t0, cur);
-    __syncthreads();
-    const u16* Ah = Sh + j * SBS + kg * 64;
-    const u16* Al = Sl + j * SBS + kg * 64;
-    for (int n = 0; n < rows_w / 32; ++n) {
-        const int t = t0 + 32 * n;
-        if (n + 1 < rows_w / 32) loadB(t + 32, nxt);
-        f32x16 acc[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-            for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            uint32_t h[4], l[4];
-            split2g(cur[2 * s].x, cur[2 * s].y, h[0], l[0]);
-            split2g(cur[2 * s].z, cur[2 * s].w, h[1], l[1]);
-            split2g(cur[2 * s + 1].x, cur[2 * s + 1].y, h[2], l[2]);
-            split2g(cur[2 * s + 1].z, cur[2 * s + 1].w, h[3], l[3]);
-            const uint4 bh = make_uint4(h[0], h[1], h[2], h[3]), bl = make_uint4(l[0], l[1], l[2], l[3]);
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const uint4 ah = *reinterpret_cast<const uint4*>(Ah + 32 * m * SBS + 8 * s);
-                const uint4 al = *reinterpret_cast<const uint4*>(Al + 32 * m * SBS + 8 * s);
-                acc[m] = mfma_bf16(ah, bh, acc[m]);
-                acc[m] = mfma_bf16(ah, bl, acc[m]);
-                acc[m] = mfma_bf16(al, bh, acc[m]);
-            }
-        }
-        // lane holds time t + j, channels 32m + 8g + 4kg + 0..3 in acc[m][4g..4g+3]
-        float* out = Ew + (size_t)(t + j) * C + 4 * kg;
-        const float* cgr = CG ? CG + (size_t)(t + j) * C + 4 * kg : nullptr;
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int c = 32 * m + 8 * g;
-                float4 o = make_float4(acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]);
-                if (cgr) {
-                    const float4 cv = *reinterpret_cast<const float4*>(cgr + c);
-                    o.x += cv.x; o.y += cv.y; o.z += cv.z; o.w += cv.w;
-                }
-                *reinterpret_cast<float4*>(out + c) = o;
-            }
-        if (n + 1 < rows_w / 32) {
-#pragma unroll
-            for (int s = 0; s < 16; ++s) cur[s] = nxt[s];
-        }
-    }
-}
-
-// Split Gatys backward, round-4 form (the default; ASTYLE_GATYS_BWD=1 the 32x32 form): v_mfma_f32_16x16x32_bf16 over
-// 16-row blocks, so a lane's E operand is 8 floats per k-step (32 registers a block) and three
-// blocks stay in flight (192 KiB per CU at two workgroups) instead of the 32x32 form's 64 floats
-// per lane and one block ahead at one wave per SIMD.  Per wave: rows t0 .. t0 + 127 in 8 blocks;
+// Split Gatys backward (round 4): v_mfma_f32_16x16x32_bf16 over 16-row blocks, so a lane's E
+// operand is 8 floats per k-step (32 registers a block) and three blocks stay in flight (192 KiB
+// per CU at two workgroups); round 3's 32x32x16 form (64 floats per lane, one block ahead at one
+// wave per SIMD) measured 28.2 against 23.9 ms per call and was removed.  Per wave: rows t0 .. t0 + 127 in 8 blocks;
 // A = S~ (symmetric: S~[c][k] = S~[k][c]) split fragments from the LDS image, row c = 16 m + (l & 15),
 // k = 32 s + 8 (l >> 4) .. + 7; B = E split from registers, lane (n = l & 15, q = l >> 4): row
 // t + n, channels 32 s + 8 q .. + 7; D lane: row t + n, channels 16 m + 4 q .. + 3 (a float4).
+// Fused content tap (a.cont_u == u, methods.py:116-117): the lane re-reads its output float4 of
+// E (in L2: the workgroup streamed the row one block earlier) and phi, adds coef (E - phi) on
+// channels < cont_ncol, and the workgroup's squared errors go to slot `tile` of the clip's
+// content partials -- k_content's 2 GiB gradient buffer, written and read back, is gone.
 typedef float f32x4g __attribute__((ext_vector_type(4)));
 constexpr int GB2 = 3;   // blocks in flight
 __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
@@ -536,6 +454,9 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
     float* Ew = (float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;   // D (in place unless out of place)
     const float* CG = (const float*)a.cg[u];
     if (CG) CG += (size_t)b * a.T * C;
+    const bool cont = u == a.cont_u;   // (workgroup-uniform)
+    const float* PH = cont ? a.cont_phi + (size_t)b * a.cont_phi_bstride + a.cont_off : nullptr;
+    float csd = 0.f;
     const int n = lane & 15, q = lane >> 4;
     const int nblk = GY_ROWS / 4 / 16;
     const int t0 = tile * GY_ROWS + w * (GY_ROWS / 4);
@@ -580,6 +501,22 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
                 const float4 cv = *reinterpret_cast<const float4*>(cgr + 16 * m);
                 o4.x += cv.x; o4.y += cv.y; o4.z += cv.z; o4.w += cv.w;
             }
+            if (cont) {
+                const int cc = 16 * m + 4 * q;
+                if (cc < a.cont_ncol) {   // (phi rows hold cont_ncol channels: quads past them load nothing)
+                    const float4 ev = *reinterpret_cast<const float4*>(E + (size_t)t * C + cc);
+                    const float4 pv = *reinterpret_cast<const float4*>(PH + (size_t)t * a.cont_ncc + cc);
+                    const float d[4] = {ev.x - pv.x, ev.y - pv.y, ev.z - pv.z, ev.w - pv.w};
+                    float dd[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        dd[i] = cc + i < a.cont_ncol ? d[i] : 0.f;
+                        csd = fmaf(dd[i], dd[i], csd);
+                    }
+                    o4.x = fmaf(a.cont_coef, dd[0], o4.x); o4.y = fmaf(a.cont_coef, dd[1], o4.y);
+                    o4.z = fmaf(a.cont_coef, dd[2], o4.z); o4.w = fmaf(a.cont_coef, dd[3], o4.w);
+                }
+            }
             *reinterpret_cast<float4*>(out + 16 * m) = o4;
         }
     };
@@ -590,6 +527,14 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
 #pragma unroll
         for (int k = 0; k < GB2; ++k)
             if (blk + k < nblk) block(vr[k], blk + k);
+    }
+    if (cont) {   // the workgroup's squared content error -> slot `tile` (fixed order: waves 0..3)
+        __shared__ float cw[4];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) csd += __shfl_xor(csd, off);
+        if (lane == 0) cw[w] = csd;
+        __syncthreads();
+        if (tid == 0) a.cont_part[(size_t)b * a.cont_pstride + tile] = ((cw[0] + cw[1]) + cw[2]) + cw[3];
     }
 }
 
@@ -688,12 +633,7 @@ void launch_gatys_bwd(const GatysArgs& a, int precision, hipStream_t s) {
     const dim3 g(a.B * a.nu * (a.T / GY_ROWS));
     if (precision == 1) hipLaunchKernelGGL(k_gatys_bwd_bf16, g, dim3(256), 0, s, a);
     else if (precision == 2) {
-        // default: the 16x16x32 three-blocks-in-flight form (round 4: 23.9 vs 28.2 ms per call
-        // at 256 clips); ASTYLE_GATYS_BWD=1 selects the 32x32x16 form (A/B; read per call)
-        const char* e = getenv("ASTYLE_GATYS_BWD");
-        const int v = e ? atoi(e) : 2;
-        if (v == 1) hipLaunchKernelGGL(k_gatys_bwd_s, g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(k_gatys_bwd_s2, g, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_gatys_bwd_s2, g, dim3(256), 0, s, a);
     }
     else hipLaunchKernelGGL(k_gatys_bwd_f32, g, dim3(256), 0, s, a);
 }

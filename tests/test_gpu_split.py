@@ -389,14 +389,16 @@ def test_range_flags(weights, dev):
     assert eng.range_flags().cpu().tolist() == [0, 0]
 
 
-def test_fused_content_tap_phi_at_buffer_end(weights, dev):
-    """the fused content tap's phi loads are masked by cnt_channels.  Per-clip phi_c of
+@pytest.mark.parametrize('gatys', [False, True])
+def test_fused_content_tap_phi_at_buffer_end(gatys, weights, dev):
+    """the fused content tap's phi loads (ours-Gram and, since round 4, Gatys backward)
+    are masked by cnt_channels.  Per-clip phi_c of
     cnt_channels 32 for 6 clips of 16384 samples is exactly 12 MiB, a caching-allocator segment of
     its own (requests >= 10 MiB are rounded to 2 MiB and not split), so on the last clip's last row
     a quad past the tap's 32 channels would read past the allocation; the split result must
     equal the fp32 kernels' to the fp32 bars."""
     B, T = 6, 16384
-    kw = dict(cont_ids=[29], style_ids=list(range(30)), gatys=False, nb_channels=128, cnt_channels=32)
+    kw = dict(cont_ids=[29], style_ids=list(range(30)), gatys=gatys, nb_channels=128, cnt_channels=32)
     xc = O.mu_law_numpy(synthetic_clips(1, T, 1000)[0])
     xs = O.mu_law_numpy(synthetic_clips(1, T, 5000)[0])
     torch.manual_seed(0)
@@ -455,13 +457,13 @@ def test_loss_grad_phases_and_clip_groups(weights, dev):
     assert torch.equal(torch.cat(grp.parts), loop.parts)
 
 
-@pytest.mark.parametrize('form', ['1', '2', '3'])
-def test_gatys_backward_forms(form, weights, golden, dev, monkeypatch):
-    """The split Gatys backward in both forms (ASTYLE_GATYS_BWD=1: 32x32x16, one block ahead;
-    2, the default: 16x16x32, three 16-row blocks in flight) against the golden 'gatys' case at the fp32 bars,
-    and at B = 3 every slot equal to that clip alone."""
-    monkeypatch.setenv('ASTYLE_GATYS_BWD', '2' if form == '2' else '1')
-    monkeypatch.setenv('ASTYLE_GATYS_STAGES', '3' if form == '3' else '2')   # form 3: the forward's third stage
+@pytest.mark.parametrize('stages', ['2', '3'])
+def test_gatys_split_kernels(stages, weights, golden, dev, monkeypatch):
+    """The split Gatys kernels (16x16x32 backward with the fused content tap; the forward with 2
+    or 3 load stages, ASTYLE_GATYS_STAGES) against the golden 'gatys' case at the fp32 bars, and
+    at B = 3 every slot equal to that clip alone."""
+    monkeypatch.setenv('ASTYLE_GATYS_STAGES', stages)
+    form = stages
     T = 2048
     x = golden['gatys_x']
     eng = _engine(1, T, CASES['gatys'], weights)
