@@ -472,6 +472,7 @@ GatysArgs gatys_args(ast_ctx* x) {
     g.gpart = x->gpart; g.smat = x->smat; g.smatb = x->smatb;
     g.B = x->cfg.batch; g.T = x->cfg.T; g.nchunk = x->nchunk;
     g.cont_u = -1;
+    g.top_u = -1; g.gmax_top = nullptr;
     return g;
 }
 
@@ -970,6 +971,12 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
         sa.smat = x->smat; sa.smatb = x->smatb; sa.spart = x->spart;
         launch_style_gatys(sa, s);
         tmark(x, s);
+        if (x->split && x->tensor_in_style[x->nblk]) {   // the chain's first max |tot| inside the Gatys bwd
+            for (int u = 0; u < x->nu; ++u) if (x->uid[u] == x->nblk) g.top_u = u;
+            g.gmax_top = x->gmax_g + (size_t)x->nblk * c.batch;
+            launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s);
+            top_max_done = g.top_u >= 0;
+        }
         if (fuse_u >= 0) {   // the split Gatys backward adds the content tap (one slot per 512-row tile)
             const Occ& o = x->occ[0];
             g.cg[fuse_u] = nullptr;

@@ -279,6 +279,8 @@ struct GatysArgs {
     int cont_ncc, cont_off, cont_ncol;
     float cont_coef;
     float* cont_part; size_t cont_pstride;
+    int top_u;                              // split bwd: tensor whose per-clip max |D| (the backward
+    unsigned* gmax_top;                     // chain's first input) goes to gmax_top[b], or -1
 };
 
 struct GatysStyleArgs {

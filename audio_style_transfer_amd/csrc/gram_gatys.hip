@@ -455,6 +455,8 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
     const float* CG = (const float*)a.cg[u];
     if (CG) CG += (size_t)b * a.T * C;
     const bool cont = u == a.cont_u;   // (workgroup-uniform)
+    const bool top = u == a.top_u;
+    float omax = 0.f;
     const float* PH = cont ? a.cont_phi + (size_t)b * a.cont_phi_bstride + a.cont_off : nullptr;
     float csd = 0.f;
     const int n = lane & 15, q = lane >> 4;
@@ -518,6 +520,7 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
                 }
             }
             *reinterpret_cast<float4*>(out + 16 * m) = o4;
+            if (top) omax = fmaxf(omax, fmaxf(fmaxf(fabsf(o4.x), fabsf(o4.y)), fmaxf(fabsf(o4.z), fabsf(o4.w))));
         }
     };
 #pragma unroll
@@ -527,6 +530,14 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
 #pragma unroll
         for (int k = 0; k < GB2; ++k)
             if (blk + k < nblk) block(vr[k], blk + k);
+    }
+    if (top) {    // the top tensor's max |D| per clip: one atomic per workgroup (no k_absmax pass)
+        __shared__ float mw[4];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) omax = fmaxf(omax, __shfl_xor(omax, off));
+        if (lane == 0) mw[w] = omax;
+        __syncthreads();
+        if (tid == 0) atomicMax(a.gmax_top + b, __float_as_uint(fmaxf(fmaxf(mw[0], mw[1]), fmaxf(mw[2], mw[3]))));
     }
     if (cont) {   // the workgroup's squared content error -> slot `tile` (fixed order: waves 0..3)
         __shared__ float cw[4];
