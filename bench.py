@@ -69,8 +69,9 @@ def parse(argv=None):
                     help='1: replay the step from a captured HIP graph (default); 0: eager launches')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=15.0,
                     help='CPU baseline sample budget (0 disables)')
-    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'traffic.json'),
-                    help='per-launch HBM bytes measured by rocprofv3 --pmc (see DESIGN.md)')
+    ap.add_argument('--traffic-json', default=None,
+                    help='per-launch HBM bytes measured by rocprofv3 --pmc (see DESIGN.md; default '
+                         'profiles/traffic.json, profiles/traffic_gatys.json with --gatys)')
     ap.add_argument('--engine', default='audio_style_transfer_amd.engine:StyleEngine',
                     help='module:Class of the engine (tests substitute a CPU stand-in)')
     ap.add_argument('--backend', default='nccl', help='torch.distributed backend for N > 1')
@@ -410,7 +411,9 @@ def rank_main(args):
     traffic = None
     sha = lib_sha16()
     try:
-        with open(args.traffic_json) as f:
+        tpath = args.traffic_json or os.path.join(
+            ROOT, 'profiles', 'traffic_gatys.json' if args.gatys else 'traffic.json')
+        with open(tpath) as f:
             tj = json.load(f)
         if (tj.get('precision') == args.precision and tj.get('clips') == Bt and tj.get('T') == T
                 and tj.get('gatys', False) == args.gatys and tj.get('lib_sha16') == sha):

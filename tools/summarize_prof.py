@@ -6,7 +6,8 @@ small side-check launches do not dilute the bench-sized ones), average duration 
 traffic per launch from the separate FETCH_SIZE / WRITE_SIZE passes.  gfx950 correction (MI355X_MICROARCH.md §HBM):
 FETCH_SIZE counts half the bytes of a wide (16 B/lane) coalesced read, so fetched bytes =
 2 * FETCH_SIZE * 1024; WRITE_SIZE reads exactly for 16-B stores: written = WRITE_SIZE * 1024.
-Also (re)writes profiles/traffic.json for bench.py's roofline.traffic field.
+Also (re)writes profiles/traffic.json (traffic_gatys.json for a --gatys profile) for bench.py's
+roofline.traffic field.
 """
 import csv
 import json
@@ -90,7 +91,7 @@ def main(tag, precision, clips, T):
               'gram_fwd_bytes_per_launch': gf.get('hbm_bytes_per_launch'),
               'gram_bwd_bytes_per_launch': gb.get('hbm_bytes_per_launch'),
               'gram_fwd_ms': gf.get('avg_ms'), 'gram_bwd_ms': gb.get('avg_ms')}
-        with open(os.path.join(dst, 'traffic.json'), 'w') as f:
+        with open(os.path.join(dst, 'traffic_gatys.json' if gatys else 'traffic.json'), 'w') as f:
             json.dump(tj, f, indent=1)
     for k, v in sorted(stats.items(), key=lambda kv: -kv[1]['total_ms'])[:10]:
         print('%-40s calls %4d avg %8.3f ms  hbm/launch %s' % (
