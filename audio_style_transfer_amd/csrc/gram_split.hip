@@ -212,10 +212,7 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_n(GramArgs a) {
 // CONT: the fused content tap (a.cont_u >= 0); false: the round-2 kernel.  NST stages of loads
 // in flight: 2 (the split of a stage into registers before the barrier) or 3 (each channel split
 // straight into the image after the barrier: 24 fewer live registers pay for the third stage)
-// DIRECT (A/B, ASTYLE_GRAM_BWD_DIRECT=1): no O image -- a lane's four accumulators at one (u, t)
-// are channels c0 + 4 w .. + 3, stored straight as a float4 (the 8 waves fill a 128-B line in
-// L2); the content tap per stored piece
-template <bool CONT, int NST, bool DIRECT = false>
+template <bool CONT, int NST>
 __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     __shared__ __attribute__((aligned(16))) u16 IH[GCS * GSS * BRS];       // [c][t][u] hi
     __shared__ __attribute__((aligned(16))) u16 IL[GCS * GSS * BRS];       // [c][t][u] lo
@@ -276,7 +273,7 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     };
     auto stage = [&](float4 (&v)[8], int t0) {
         float4 ce, cph = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (CONT && cthr && !DIRECT) {
+        if (CONT && cthr) {
             ce = *reinterpret_cast<const float4*>(ce_src + (size_t)(t0 + ctt) * C);
             // phi rows hold only the tap's cont_ncol (a multiple of 4) channels: quads past them
             // load nothing (the row's last quad can end the caller's buffer)
@@ -321,49 +318,6 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
             return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][0]),
                                                           __builtin_bit_cast(bf16x8, bl), c, 0, 0, 0);
         };
-        if (DIRECT) {
-#pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                f32x4 acc[4];
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc) acc[cc] = dhalf(m, cc);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int u = 16 * m + 4 * kq + i;
-                    if (u < a.nu) {
-                        const int t = t0 + i16;
-                        float4 o = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
-                        const size_t rowc = ((size_t)b * a.T + t) * C + c0 + 4 * w;
-                        const size_t off = (size_t)a.uid[u] * a.tstride + rowc;
-                        const float* cg = (const float*)a.cg[u];
-                        if (cg) {
-                            const float4 g = *reinterpret_cast<const float4*>(cg + rowc);
-                            o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
-                        }
-                        if (CONT && u == a.cont_u) {
-                            const int cc0 = c0 + 4 * w;
-                            const float4 e4 = *reinterpret_cast<const float4*>((const float*)a.act + off);
-                            float4 p4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                            if (cc0 < a.cont_ncol)
-                                p4 = *reinterpret_cast<const float4*>(a.cont_phi + (size_t)b * a.cont_phi_bstride + a.cont_off + (size_t)t * a.cont_ncc + cc0);
-                            const float ev[4] = {e4.x, e4.y, e4.z, e4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
-                            float d[4];
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) {
-                                d[k] = cc0 + k < a.cont_ncol ? ev[k] - pv[k] : 0.f;
-                                csd = fmaf(d[k], d[k], csd);
-                            }
-                            o.x += a.cont_coef * d[0]; o.y += a.cont_coef * d[1];
-                            o.z += a.cont_coef * d[2]; o.w += a.cont_coef * d[3];
-                        }
-                        *reinterpret_cast<float4*>((float*)a.actw + off) = o;
-                        if (u == a.top_u)
-                            omax = fmaxf(omax, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
-                    }
-                }
-            }
-            return;
-        }
         float4 cadd = make_float4(0.f, 0.f, 0.f, 0.f);
         if (CONT && cthr) {
             const int cc = c0 + 4 * cq;
@@ -758,13 +712,6 @@ void launch_gram_bwd_s(const GramArgs& a, hipStream_t s) {
     if (a.cont_u >= 0 && (a.T / a.nchunk) % GRAM_CSLOT) {
         fprintf(stderr, "gram_bwd_s: the fused content tap needs whole %d-row chunks\n", GRAM_CSLOT);
         abort();
-    }
-    static int direct = -1;
-    if (direct < 0) { const char* e = getenv("ASTYLE_GRAM_BWD_DIRECT"); direct = e && atoi(e) ? 1 : 0; }
-    if (direct) {
-        if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 2, true>), grid, dim3(GWT), 0, s, a);
-        else hipLaunchKernelGGL((k_gram_bwd_s<false, 2, true>), grid, dim3(GWT), 0, s, a);
-        return;
     }
     if (gram_bwd_stages() == 3) {
         if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 3>), grid, dim3(GWT), 0, s, a);
