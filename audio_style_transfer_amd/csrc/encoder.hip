@@ -251,13 +251,21 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
     // workgroups belong to different clips, so their max atomics do not pile onto one word
     const int nper = T / SFR;
     const size_t lb = (size_t)(blockIdx.x % B) * nper + blockIdx.x / B;
+    // the workgroup's SFR samples and their two neighbours, one coalesced load (zero past the clip)
+    __shared__ float xs[SFR + 2];
+    {
+        const int t0 = (int)((lb * SFR) % T);
+        const float* xc = x + (lb * SFR - t0);   // the clip's first sample
+        for (int i = threadIdx.x; i < SFR + 2; i += 256) {
+            const int t = t0 - 1 + i;
+            xs[i] = t >= 0 && t < T ? xc[t] : 0.f;
+        }
+    }
+    __syncthreads();
     for (int it = 0; it < SFR / 16; ++it) {
-        const size_t rowi = lb * SFR + it * 16 + (threadIdx.x >> 4);
-        const int t = (int)(rowi % T);
-        const float* xr = x + (rowi - t);
-        const float xm = t > 0 ? xr[t - 1] : 0.f;
-        const float x0 = xr[t];
-        const float xp = t < T - 1 ? xr[t + 1] : 0.f;
+        const int r = it * 16 + (threadIdx.x >> 4);   // row within the workgroup's SFR
+        const size_t rowi = lb * SFR + r;
+        const float xm = xs[r], x0 = xs[r + 1], xp = xs[r + 2];
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = e0_val(wk[0][j], wk[1][j], wk[2][j], bk[j], xm, x0, xp);
