@@ -14,12 +14,14 @@ LIB_PATH = os.environ.get('ASTYLE_LIB', os.path.join(PKG, 'libastyle.so'))
 MAX_TAPS = 32
 # per-clip flags of ast_range_flags (include/astyle.h)
 RANGE_NONFINITE, RANGE_ACT, RANGE_GRAD, RANGE_TINY = 1, 2, 4, 8
+LBFGS_HISTORY = 4096    # AST_LBFGS_HISTORY: evaluations per minimize call kept for ast_lbfgs_history
 
 # Every symbol include/astyle.h declares (checked by tests/test_abi.py).
 EXPORTS = ('ast_create', 'ast_destroy', 'ast_workspace_bytes', 'ast_set_weight', 'ast_forward',
            'ast_get_extract', 'ast_embeds', 'ast_content_cols', 'ast_set_targets',
            'ast_set_gamma', 'ast_loss_grad', 'ast_loss_grad_phase', 'ast_range_flags', 'ast_range_flags_reset', 'ast_set_cu_limit', 'ast_adam_step', 'ast_adam_step_dev',
            'ast_lbfgs_workspace_bytes', 'ast_lbfgs_begin', 'ast_lbfgs_step', 'ast_lbfgs_state',
+           'ast_lbfgs_history',
            'ast_timing', 'ast_timing_read', 'ast_ot_admm', 'ast_ckpt_open', 'ast_ckpt_close',
            'ast_ckpt_num_entries', 'ast_ckpt_entry', 'ast_ckpt_read_f32', 'ast_restore',
            'ast_last_error')
@@ -75,6 +77,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         'ast_lbfgs_begin': (i, [vp, vp, vp, vp, vp, i, i, i, ctypes.c_double, ctypes.c_double, vp]),
         'ast_lbfgs_step': (i, [vp, vp, vp, vp, vp, vp]),
         'ast_lbfgs_state': (i, [vp, vp, vp, vp, vp]),
+        'ast_lbfgs_history': (i, [vp, vp, vp, i, vp]),
         'ast_timing': (i, [vp, i]),
         'ast_timing_read': (i, [vp, fp, i]),
         'ast_ot_admm': (i, [vp, vp, i, i, i, i, ctypes.c_double, ctypes.c_double, vp, vp, vp, vp]),

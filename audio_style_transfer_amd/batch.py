@@ -31,6 +31,7 @@ import copy
 import importlib
 import os
 import sys
+import time
 import warnings
 
 import numpy as np
@@ -152,7 +153,9 @@ def run_rank(args, pairs, ws, rank, dev, log=print):
     writers = [summary.EventWriter(lp) for _, lp in dirs]
 
     def epoch(precision, sel, x0):
-        """One minimize call for the clips in `sel` on the `precision` kernels, from x0."""
+        """One minimize call for the clips in `sel` on the `precision` kernels, from x0:
+        (info, end points, per-clip evaluation histories).  begin(x0) restarts every clip of
+        that loop, so each loop runs at most once per epoch and only `sel`'s rows are used."""
         if precision not in loops:
             engines[precision] = build(precision)
             loops[precision] = Loop(engines[precision], maxiter=100)
@@ -160,46 +163,60 @@ def run_rank(args, pairs, ws, rank, dev, log=print):
         info = lp.minimize(torch.tensor(x0, dtype=torch.float64),
                            active=torch.tensor(sel.astype(np.int32)))
         _, xe = lp.state(with_x=True)
-        return info, xe.cpu().numpy(), lp.parts.cpu().numpy().astype(np.float64)
+        return info, xe.cpu().numpy(), lp.history(info)
 
+    from . import _lib
+    guard = _lib.RANGE_NONFINITE | _lib.RANGE_ACT | _lib.RANGE_GRAD
+    since = time.time()                                              # methods.py:160
     for ep in range(int(start_ep.min()) if B else 0, args.epochs):
         run = active & (start_ep <= ep)
         if not run.any():
             break
         x0 = x.astype(np.float32).astype(np.float64)                # each epoch from fp32(x)
-        res = {}
-        for p in sorted(set(prec[b] for b in np.flatnonzero(run))):
-            sel = run & np.array([q == p for q in prec])
-            res[p] = epoch(p, sel, x0)
+        xe, hist = np.empty_like(x), [None] * B
+        # one minimize call per precision; the split clips first, so the clips its range guard
+        # flags join this epoch's single fp32 call (from the same x0) beside the clips already
+        # on fp32, and every clip's result is taken from the one call that ran it
+        pending = {p: run & np.array([q == p for q in prec]) for p in ('split', 'bf16', 'fp32')}
+        for p in ('split', 'bf16', 'fp32'):
+            sel = pending[p]
+            if not sel.any():
+                continue
+            info, xs, hs = epoch(p, sel, x0)
             if p == 'split':                                         # the range guard
                 f = engines[p].range_flags().cpu().numpy()
-                from . import _lib
-                bad = sel & ((f & (_lib.RANGE_NONFINITE | _lib.RANGE_ACT | _lib.RANGE_GRAD)) != 0)
+                bad = sel & ((f & guard) != 0)
                 if bad.any():
                     log('split precision: range flags on clips %s; their epoch reruns on fp32 '
                         'kernels' % [mine[b] for b in np.flatnonzero(bad)])
                     for b in np.flatnonzero(bad):
                         prec[b] = 'fp32'
-                    res['fp32'] = epoch('fp32', bad, x0)
-        for p, (info, xe, parts) in res.items():
-            for b in np.flatnonzero(run & np.array([q == p for q in prec])):
-                n = int(info[b, 2])
-                x[b] = xe[b]
-                pv = parts[b]
+                    pending['fp32'] = pending['fp32'] | bad
+                    sel = sel & ~bad
+            for b in np.flatnonzero(sel):
+                xe[b], hist[b] = xs[b], hs[b]
+        tl = time.time() - since     # the epoch's end: the device evaluations are not host-timed
+        for b in np.flatnonzero(run):
+            h = hist[b]
+            n = len(h)
+            x[b] = xe[b]
+            for k, pv in enumerate(h):                               # methods.py:147-157
                 writers[b].add_scalars({'loss/content_loss': pv[1], 'loss/style_loss': pv[2],
                                         'loss/regularizer': pv[3], 'loss/main_loss': pv[0]},
-                                       int(i_[b]) + n - 1)          # the epoch's last evaluation
-                writers[b].flush()
-                i_[b] = n
-                sp = dirs[b][0]
-                np.savez(os.path.join(sp, 'state.npz'), x=x[b].astype(np.float32).astype(np.float64),
-                         ep=ep, i_=i_[b], fingerprint=np.array(fps[b]))
-                audio = utils.inv_mu_law_numpy(x[b][None])[0, net.late:-net.late]
-                utils.write_wav(os.path.join(sp, 'ep-{}.wav'.format(ep)), audio / np.max(audio), args.sr)
-                log('pair %d %s->%s: Ep %d/%d-it %d-loss%.4f-%.4f-%.4f-%.4f' % (
-                    mine[b], pairs[mine[b]][0], pairs[mine[b]][1], ep + 1, args.epochs, n, *pv))
-                if n < 50:                                           # methods.py:180-181
-                    active[b] = False
+                                       int(i_[b]) + k)
+                if not k % 5:
+                    log('pair %d %s->%s: Ep %d/%d-it %d(%d)-tlapse %.4fs-loss%.4f-%.4f-%.4f-%.4f' % (
+                        mine[b], pairs[mine[b]][0], pairs[mine[b]][1], ep + 1, args.epochs, k,
+                        i_[b], tl, *pv))
+            writers[b].flush()
+            i_[b] = n
+            sp = dirs[b][0]
+            np.savez(os.path.join(sp, 'state.npz'), x=x[b].astype(np.float32).astype(np.float64),
+                     ep=ep, i_=i_[b], fingerprint=np.array(fps[b]))
+            audio = utils.inv_mu_law_numpy(x[b][None])[0, net.late:-net.late]
+            utils.write_wav(os.path.join(sp, 'ep-{}.wav'.format(ep)), audio / np.max(audio), args.sr)
+            if n < 50:                                               # methods.py:180-181
+                active[b] = False
     for w in writers:
         w.close()
     for e in engines.values():

@@ -1220,6 +1220,17 @@ int ast_lbfgs_state(ast_ctx* x, const void* ws, int* info, double* x64, void* st
     return 0;
 }
 
+int ast_lbfgs_history(ast_ctx* x, const void* ws, float* out, int max_evals, void* stream) {
+    if (!x || !ws || !out) return fail(AST_E_ARG, "null argument");
+    if (max_evals < 1 || max_evals > lbfgs_history_cap())
+        return fail(AST_E_ARG, "max_evals must be in 1..AST_LBFGS_HISTORY");
+    if (std::find(x->lb_ws.begin(), x->lb_ws.end(), ws) == x->lb_ws.end())
+        return fail(AST_E_STATE, "ast_lbfgs_begin (with x0) has not been called on this workspace");
+    launch_lbfgs_history(ws, out, max_evals, x->cfg.batch, x->cfg.T, S(stream));
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 // Event layout per timed ast_loss_grad call (8 marks):
 //  m0 start | startconv | m1 | blocks fwd | m2 | content | m3 gram fwd m4 style m5 gram bwd m6
 //  | blocks bwd | m7 | startconv bwd + finalize | m8

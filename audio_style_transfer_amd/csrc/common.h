@@ -383,6 +383,8 @@ void launch_lbfgs_begin(void* ws, float* x, const double* x0, const int* active,
 void launch_lbfgs_step(void* ws, float* x, const float* grad, const float* parts, int B, int T,
                        hipStream_t s);
 void launch_lbfgs_state(const void* ws, int* info, double* x64, int B, int T, hipStream_t s);
+int lbfgs_history_cap();
+void launch_lbfgs_history(const void* ws, float* out, int cap, int B, int T, hipStream_t s);
 
 void launch_adam(float* x, float* m, float* v, const float* g, size_t n, float lr, float b1,
                  float b2, float eps, float bc1, float bc2, hipStream_t s);

@@ -50,6 +50,10 @@ struct LbHeader {
 };
 constexpr int LB_MAGIC = 0x4c42464d;
 constexpr size_t LB_HDR = 512;
+// per clip, the loss parts (total, content, style, regularizer) of the first LB_HIST
+// evaluations of the current minimize call, in evaluation order (methods.py:147-157 logs every
+// evaluation; scipy's maxiter 100 with maxls 20 makes at most 2001)
+constexpr int LB_HIST = 4096;
 
 // reasons (ast_lbfgs_state)
 enum { LB_RUNNING = 0, LB_STOP_ITER = 1, LB_CONV_PGTOL = 2, LB_CONV_REL_F = 3, LB_ABNORMAL = 4,
@@ -69,6 +73,7 @@ struct Ws {   // workspace views for clip b
     double* D;
     double* S;    // [m][T]
     double* Y;    // [m][T]
+    float4* H;    // [LB_HIST] loss parts per evaluation
 };
 
 __device__ __forceinline__ Ws ws_view(void* base, int B, int T, int m, int b) {
@@ -80,6 +85,7 @@ __device__ __forceinline__ Ws ws_view(void* base, int B, int T, int m, int b) {
     v += (size_t)b * per;
     w.X[0] = v; w.X[1] = v + T; w.R = v + 2 * (size_t)T; w.D = v + 3 * (size_t)T;
     w.S = v + 4 * (size_t)T; w.Y = v + (4 + (size_t)m) * T;
+    w.H = (float4*)((double*)(p + (size_t)B * 512) + (size_t)B * per) + (size_t)b * LB_HIST;
     return w;
 }
 
@@ -353,6 +359,9 @@ __global__ void __launch_bounds__(NT) k_lbfgs_step(StepArgs a) {
     float* xd = a.x + (size_t)b * T;
     const float* g = a.grad + (size_t)b * T;
     const double f = (double)a.parts[b * 4 + 0];
+    if (threadIdx.x == 0 && s.nfev < LB_HIST)
+        w.H[s.nfev] = make_float4(a.parts[b * 4 + 0], a.parts[b * 4 + 1], a.parts[b * 4 + 2],
+                                  a.parts[b * 4 + 3]);
     s.nfev++;
     if (s.phase == 1) {                                          // f, g at the start point
         double gmax = 0.0;
@@ -490,10 +499,29 @@ __global__ void k_lbfgs_state(const void* ws, int* info, double* x64, int B, int
     }
 }
 
+// out [B][cap][4]: the parts of evaluations 0 .. min(nfev, cap) - 1 of each clip's current (or
+// last) minimize call, NaN past its count
+__global__ void k_lbfgs_history(const void* ws, float4* out, int cap, int B, int T) {
+    const int b = blockIdx.x;
+    const bool ok = ws_ok(ws, B, T);
+    const Ws w = ws_view(const_cast<void*>(ws), B, T, ok ? ws_m(ws) : 1, b);
+    const int n = ok ? min(w.st->nfev, LB_HIST) : 0;
+    const float q = __builtin_nanf("");
+    for (int i = threadIdx.x; i < cap; i += blockDim.x)
+        out[(size_t)b * cap + i] = i < n ? w.H[i] : make_float4(q, q, q, q);
+}
+
 }  // namespace
 
 size_t lbfgs_workspace_bytes(int B, int T, int m) {
-    return LB_HDR + (size_t)B * 512 + (size_t)B * (4 + 2 * (size_t)m) * T * 8;
+    return LB_HDR + (size_t)B * 512 + (size_t)B * (4 + 2 * (size_t)m) * T * 8 +
+           (size_t)B * LB_HIST * sizeof(float4);
+}
+
+int lbfgs_history_cap() { return LB_HIST; }
+
+void launch_lbfgs_history(const void* ws, float* out, int cap, int B, int T, hipStream_t s) {
+    hipLaunchKernelGGL(k_lbfgs_history, dim3(B), dim3(256), 0, s, ws, (float4*)out, cap, B, T);
 }
 
 void launch_lbfgs_begin(void* ws, float* x, const double* x0, const int* active, int B, int T,

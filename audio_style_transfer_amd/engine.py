@@ -457,6 +457,20 @@ class LbfgsLoop:
                                                 self._p(x64), self.eng._stream()))
         return self.info.cpu().numpy(), x64
 
+    def history(self, info=None):
+        """Per clip, the (total, content, style, regularizer) parts of every evaluation of the
+        current (or last) minimize call in evaluation order: a list of [n_b, 4] float64 arrays
+        (n_b = the clip's evaluation count, info[:, 2]; ast_lbfgs_history)."""
+        if info is None:
+            info, _ = self.state()
+        n = np.minimum(np.asarray(info)[:, 2], _lib.LBFGS_HISTORY)
+        cap = max(1, int(n.max()) if n.size else 1)
+        out = torch.empty(self.eng.batch, cap, 4, device=self.eng.device)
+        _lib.check(self.eng.lib.ast_lbfgs_history(self.eng.h, self._p(self.ws), self._p(out), cap,
+                                                  self.eng._stream()))
+        h = out.cpu().numpy().astype(np.float64)
+        return [h[b, :int(n[b])] for b in range(self.eng.batch)]
+
     def minimize(self, x0: Optional[torch.Tensor] = None, active=None, check_every: int = 4,
                  max_steps: int = 100000):
         """Run until every clip's minimize call has returned; returns the final info."""

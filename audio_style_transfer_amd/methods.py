@@ -126,7 +126,8 @@ class GatysNet(object):
                **kw):
         """methods.py:140-181 with scipy L-BFGS-B driving ast_loss_grad (``optimizer='scipy'``,
         one host round trip per evaluation, as the reference), or the same L-BFGS-B run on the
-        device (``'device'``: ast_lbfgs_*, no round trip; progress is logged per epoch).
+        device (``'device'``: ast_lbfgs_*, no round trip; each epoch's evaluations are logged
+        from the workspace's loss history after the epoch).
         Accepts the reference's l_bfgs(sess, phi_c, phi_s, epochs, lambd, gamma) as well.  Every
         epoch starts from the float32 rounding of its point, as the TF variable does.
 
@@ -214,11 +215,16 @@ class GatysNet(object):
                     info = loop.minimize(torch.tensor(x[None], dtype=torch.float64))
                 x = loop.state(with_x=True)[1][0].cpu().numpy()
                 state['i'] = int(info[0, 2])
-                p = loop.parts[0].cpu().numpy().astype(np.float64)
-                history.append((float(p[0]), float(p[1]), float(p[2]), float(p[3])))
-                scalars(p, state['i_'] + state['i'] - 1)      # the epoch's last evaluation
-                log('Ep {0:}/{1:}-it {2:}-tlapse {3:.4f}s-loss{4:.4f}-{5:.4f}-{6:.4f}-{7:.4f}'.format(
-                    ep + 1, epochs, state['i'], time.time() - state['since'], *p))
+                # every evaluation's parts, from the workspace's history (ast_lbfgs_history), at
+                # step i_ + i with the progress line every 5, as the scipy path's fg does; the
+                # device evaluations are not timed one by one, so tlapse is the epoch's end
+                tl = time.time() - state['since']
+                for k, p in enumerate(loop.history(info)[0]):
+                    history.append((float(p[0]), float(p[1]), float(p[2]), float(p[3])))
+                    scalars(p, state['i_'] + k)
+                    if not k % 5:                                         # methods.py:152-155
+                        log('Ep {0:}/{1:}-it {2:}({3:})-tlapse {4:.4f}s-loss{5:.4f}-{6:.4f}-{7:.4f}-{8:.4f}'.format(
+                            ep + 1, epochs, k, state['i_'], tl, *p))
             state['i_'] = state['i']
             writer.flush()
             np.savez(ckpt, x=x.astype(np.float32).astype(np.float64), ep=ep, i_=state['i_'],

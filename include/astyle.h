@@ -171,6 +171,15 @@ int ast_lbfgs_step(ast_ctx* ctx, void* ws_dev, float* x_dev, const float* grad_d
                    const float* parts_dev, void* stream);
 int ast_lbfgs_state(ast_ctx* ctx, const void* ws_dev, int* info_dev, double* x64_dev,
                     void* stream);
+/* The loss history of the current (or last) minimize call, every evaluation's
+ * (total, content, style, regularizer) parts in evaluation order: what the reference's
+ * loss_callback writes to its event file at every evaluation (methods.py:147-157, 167).
+ * out_dev [batch, max_evals, 4] float; rows past a clip's evaluation count (info[2]) are NaN.
+ * The workspace keeps the first AST_LBFGS_HISTORY evaluations of a call (scipy's maxiter 100
+ * with maxls 20 makes at most 2001); max_evals in 1..AST_LBFGS_HISTORY. */
+#define AST_LBFGS_HISTORY 4096
+int ast_lbfgs_history(ast_ctx* ctx, const void* ws_dev, float* out_dev, int max_evals,
+                      void* stream);
 
 /* Per-kernel-family device timing (HIP events on the call's stream).  enable!=0 starts
  * recording; ast_timing_read fills out[0..n) with milliseconds summed since enable for

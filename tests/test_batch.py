@@ -93,3 +93,61 @@ def test_two_rank_batch_matches_one_rank(tmp_path):
     assert sorted(l1) == sorted(l2) and len(l1) == 3
     for k in l1:
         assert l1[k] == l2[k] and len(l1[k]) >= 1, (k, l1[k], l2[k])
+
+
+def _run_env(tmp, tag, pairs, engine, extra_env, epochs=3):
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(ROOT, 'tests'), ROOT]))
+    env.pop('WORLD_SIZE', None)
+    env.update(extra_env)
+    cmd = [sys.executable, '-m', 'audio_style_transfer_amd.batch', '--pairs', pairs,
+           '--gpus', '1', '--engine', engine, '--backend', 'gloo', '--precision', 'split',
+           '--batch_size', '4096', '--epochs', str(epochs), '--no_plots', '--stack', '0',
+           '--dir', os.path.join(tmp, 'src'), '--outdir', os.path.join(tmp, 'out_' + tag),
+           '--logdir', os.path.join(tmp, 'log_' + tag)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def test_range_guard_fallbacks_in_two_epochs_keep_every_clip_result(tmp_path):
+    """VERDICT r4 weak #5 / ADVICE r4 high: clip 0 is flagged in epoch 0 and clip 1 in epoch 1.
+    In epoch 1 clip 0 already runs on fp32 when clip 1 joins it; each fp32 clip must run once
+    from the epoch's start point and keep its own result, evaluation count and activity.  The
+    stand-in's problem does not depend on the precision, so every pair's outputs (wavs, states,
+    every evaluation's event scalars and steps) must equal an unflagged run's, and pair 0's must
+    equal its own single-pair run's."""
+    tmp = str(tmp_path)
+    _wavs(os.path.join(tmp, 'src'))
+    pairs = os.path.join(tmp, 'pairs.txt')
+    with open(pairs, 'w') as f:
+        f.write('a b\nb c\nc a\n')
+    eng = 'bench_stub:IllCondStubEngine'
+    log = _run_env(tmp, 'flag', pairs, eng, {'STUB_RANGE_FLAGS': '0:0,1:1'})
+    _run_env(tmp, 'ref', pairs, eng, {'STUB_RANGE_FLAGS': ''})
+    _run_env(tmp, 'one', 'a:b', eng, {'STUB_RANGE_FLAGS': ''})
+    assert 'range flags on clips [0]' in log and 'range flags on clips [1]' in log
+    of, orf = _collect(os.path.join(tmp, 'out_flag')), _collect(os.path.join(tmp, 'out_ref'))
+    lf, lr = _collect(os.path.join(tmp, 'log_flag')), _collect(os.path.join(tmp, 'log_ref'))
+    o1, l1 = _collect(os.path.join(tmp, 'out_one')), _collect(os.path.join(tmp, 'log_one'))
+    assert sorted(of) == sorted(orf) and len({k.split(os.sep)[0] for k in of}) == 3
+    for d in {k.split(os.sep)[0] for k in of}:      # every pair ran all 3 epochs (no early stop)
+        assert os.path.join(d, 'ep-2.wav') in of, sorted(of)
+    for k in orf:
+        if isinstance(orf[k], dict):
+            for kk in orf[k]:
+                assert np.array_equal(of[k][kk], orf[k][kk]), (k, kk)
+        else:
+            assert np.array_equal(of[k], orf[k]), k
+    assert sorted(lf) == sorted(lr)
+    for k in lr:
+        assert lf[k] == lr[k], k
+        steps = [s for s, sc in lr[k] if sc]
+        assert len(steps) > 150                      # every evaluation of 3 epochs is logged
+    for k in o1:                                     # pair 0 alone
+        ref = orf[k]
+        if isinstance(ref, dict):
+            assert all(np.array_equal(o1[k][kk], ref[kk]) for kk in ref), k
+        else:
+            assert np.array_equal(o1[k], ref), k
+    for k in l1:
+        assert l1[k] == lr[k], k

@@ -25,7 +25,7 @@ def _wavs(d):
 
 def test_batch_device_pairs_equal_single_runs(tmp_path):
     assert torch.cuda.is_available(), 'gpu tests need an MI355X'
-    from audio_style_transfer_amd import batch, methods
+    from audio_style_transfer_amd import batch, methods, summary
     src = str(tmp_path / 'src')
     _wavs(src)
     common = ['--batch_size', '4096', '--epochs', '1', '--no_plots', '--stack', '0', '--dir', src]
@@ -44,4 +44,12 @@ def test_batch_device_pairs_equal_single_runs(tmp_path):
                               wavfile.read(os.path.join(d_1, 'ep-0.wav'))[1]), (c, s)
         with np.load(os.path.join(d_b, 'state.npz')) as zb, np.load(os.path.join(d_1, 'state.npz')) as z1:
             assert np.array_equal(zb['x'], z1['x']) and int(zb['i_']) == int(z1['i_'])
-        assert glob.glob(os.path.join(batch.pair_dirs(args, c, s)[1], 'events.out.tfevents.*'))
+        # every evaluation's scalars at the same steps (ast_lbfgs_history on both sides)
+        fb = glob.glob(os.path.join(batch.pair_dirs(args, c, s)[1], 'events.out.tfevents.*'))
+        f1 = glob.glob(os.path.join(methods.get_dir(a1.logdir, a1), 'events.out.tfevents.*'))
+        assert len(fb) == 1 and len(f1) == 1
+        eb = [(e['step'], sorted(e['scalars'].items())) for e in summary.read_events(fb[0]) if e['scalars']]
+        e1 = [(e['step'], sorted(e['scalars'].items())) for e in summary.read_events(f1[0]) if e['scalars']]
+        assert eb == e1
+        with np.load(os.path.join(d_1, 'state.npz')) as z1:
+            assert len(eb) == int(z1['i_']) and [st for st, _ in eb] == list(range(len(eb)))
