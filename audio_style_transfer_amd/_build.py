@@ -37,13 +37,32 @@ EXTRA = {'block_fwd_bf16.hip': _CW, 'block_bwd_bf16.hip': _CW, 'block_fwd_split.
          'block_fwd_winoprobe.hip': _CW, 'block_bwd_winoprobe.hip': _CW}
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def _stale(lib: str = LIB, extra=()) -> bool:
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    t = os.path.getmtime(lib)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + list(extra)
     deps.append(os.path.join(os.path.dirname(PKG), 'include', 'astyle.h'))
+    deps.append(os.path.abspath(__file__))
     return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_variant(name: str = 'fwdvariants', force: bool = False) -> str:
+    """The tools-only A/B library libastyle_<name>.so of VARIANT_SOURCES[name], rebuilt from the
+    committed sources whenever they changed (tests/test_gpu_roles.py loads it)."""
+    lib = os.path.join(PKG, 'libastyle_%s.so' % name)
+    extra = [os.path.join(VARIANTS, f) for f in VARIANT_SOURCES.get(name, ([], []))[0]]
+    if not force and not _stale(lib, extra):
+        return lib
+    old = os.environ.get('ASTYLE_VARIANT')
+    os.environ['ASTYLE_VARIANT'] = name
+    try:
+        return build(force=True)
+    finally:
+        if old is None:
+            del os.environ['ASTYLE_VARIANT']
+        else:
+            os.environ['ASTYLE_VARIANT'] = old
 
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:

@@ -19,7 +19,7 @@ LBFGS_HISTORY = 4096    # AST_LBFGS_HISTORY: evaluations per minimize call kept 
 # Every symbol include/astyle.h declares (checked by tests/test_abi.py).
 EXPORTS = ('ast_create', 'ast_destroy', 'ast_workspace_bytes', 'ast_set_weight', 'ast_forward',
            'ast_get_extract', 'ast_embeds', 'ast_content_cols', 'ast_set_targets',
-           'ast_set_gamma', 'ast_loss_grad', 'ast_loss_grad_phase', 'ast_range_flags', 'ast_range_flags_reset', 'ast_set_cu_limit', 'ast_adam_step', 'ast_adam_step_dev',
+           'ast_set_gamma', 'ast_loss_grad', 'ast_loss_grad_phase', 'ast_range_flags', 'ast_range_flags_last', 'ast_range_flags_reset', 'ast_set_cu_limit', 'ast_adam_step', 'ast_adam_step_dev',
            'ast_lbfgs_workspace_bytes', 'ast_lbfgs_begin', 'ast_lbfgs_step', 'ast_lbfgs_state',
            'ast_lbfgs_history',
            'ast_timing', 'ast_timing_read', 'ast_ot_admm', 'ast_ckpt_open', 'ast_ckpt_close',
@@ -69,6 +69,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         'ast_loss_grad': (i, [vp, vp, vp, vp, vp]),
         'ast_loss_grad_phase': (i, [vp, vp, vp, vp, i, vp]),
         'ast_range_flags': (i, [vp, vp, vp]),
+        'ast_range_flags_last': (i, [vp, vp, vp]),
         'ast_range_flags_reset': (i, [vp, vp]),
         'ast_set_cu_limit': (i, [vp, i]),
         'ast_adam_step': (i, [vp, vp, vp, vp, vp, i, f, f, f, f, vp]),

@@ -133,6 +133,7 @@ struct ast_ctx {
     std::vector<const void*> lb_ws;         // workspaces started here with x0 (ast_lbfgs_begin)
     void* zero = nullptr;                   // 256 zero bytes
     int* rflags = nullptr;                  // [B] AST_RANGE_* OR'ed over ast_loss_grad calls since the last reset
+    int* rflags_last = nullptr;             // [B] AST_RANGE_* of the last ast_loss_grad alone
     size_t gpart_elems = 0, smat_elems = 0; // per context (mode-dependent)
     int ncpart = 0;
     std::vector<void*> allocs;
@@ -348,6 +349,7 @@ u16* blkwb(ast_ctx* x, int l) { return x->wtsb + (size_t)l * BLKB_SZ; }
 void* tens(ast_ctx* x, int t) { return (char*)x->act + (size_t)t * x->tstride * x->esz; }
 
 int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
+    x->lg_front_done = false;   // phase 1's state (act, gmax) is about to be overwritten
     const ast_cfg& c = x->cfg;
     if (x->split) {
         launch_zero32(x->gmax_e, (size_t)(NBLK_MAX + 1) * c.batch * 4, s);
@@ -679,6 +681,8 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     (void)hipMemset(x->zero, 0, 256);
     ALLOC(x->rflags, (size_t)c.batch * 4);
     (void)hipMemset(x->rflags, 0, (size_t)c.batch * 4);
+    ALLOC(x->rflags_last, (size_t)c.batch * 4);
+    (void)hipMemset(x->rflags_last, 0, (size_t)c.batch * 4);
     ALLOC(x->spart, (size_t)c.batch * C * 4);
     x->ncpart = (int)x->occ.size() * (c.T / CROWS);
     ALLOC(x->cpart, (size_t)c.batch * x->ncpart * 4);
@@ -914,12 +918,14 @@ int ast_set_targets(ast_ctx* x, const float* phi_c, int phi_c_shared, const floa
     x->phi_c = phi_c; x->phi_c_shared = phi_c_shared;
     x->phi_s = phi_s; x->phi_s_shared = phi_s_shared;
     x->targets = true;
+    x->lg_front_done = false;   // a phase 2 must follow a phase 1 of these targets
     return 0;
 }
 
 int ast_set_gamma(ast_ctx* x, float gamma) {
     if (!x) return fail(AST_E_ARG, "null argument");
     x->cfg.gamma = gamma;
+    x->lg_front_done = false;
     return 0;
 }
 
@@ -1019,6 +1025,7 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
     }
     tmark(x, s);
     x->lg_front_done = true;
+    x->fwd_done = false;   // the Gram backward wrote D over the tapped tensors (in place)
     return 0;
 }
 
@@ -1111,6 +1118,7 @@ static int loss_grad_back(ast_ctx* x, const float* xd, float* grad, float* parts
         ra.split = x->split; ra.nblk = x->nblk; ra.B = c.batch; ra.T = c.T;
         for (int l = 0; l < NBLK_MAX; ++l) { ra.wdn[l] = x->wdn[l]; ra.bdm[l] = x->bdm[l]; ra.wrn[l] = x->wrn[l]; }
         ra.flags = x->rflags;
+        ra.last = x->rflags_last;
         launch_range_flags(ra, s);
     }
     tmark(x, s);
@@ -1144,6 +1152,12 @@ int ast_loss_grad_phase(ast_ctx* x, const float* xd, float* grad, float* parts, 
 int ast_range_flags(ast_ctx* x, int* flags, void* stream) {
     if (!x || !flags) return fail(AST_E_ARG, "null argument");
     HIPCHK(hipMemcpyAsync(flags, x->rflags, (size_t)x->cfg.batch * 4, hipMemcpyDeviceToDevice, S(stream)));
+    return 0;
+}
+
+int ast_range_flags_last(ast_ctx* x, int* flags, void* stream) {
+    if (!x || !flags) return fail(AST_E_ARG, "null argument");
+    HIPCHK(hipMemcpyAsync(flags, x->rflags_last, (size_t)x->cfg.batch * 4, hipMemcpyDeviceToDevice, S(stream)));
     return 0;
 }
 

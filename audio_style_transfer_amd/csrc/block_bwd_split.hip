@@ -46,8 +46,12 @@ constexpr int LA = 2;                 // B-fragment lookahead (steps)
 // epilogue -- out = d loss / d e_0 is not stored; per position the wave's three dot products
 // sum_c W0[k][c] out[t][c] over its 32 channels go to spart (launch_startx_gx sums the four
 // waves and forms d loss / d x): no 2 GiB g_0 round trip (model.py:82-93)
-template <bool MASKED, bool ONESEG, bool HAS_D, bool SX>
+// WHOLE (one-segment layout with n == 64: every tile is a whole sub-sequence, d = T / 64): both
+// halo rows (p0 - 1, p0 + 64) are SAME padding, so the column tiles cover p0 .. p0 + 63 and rows
+// 0 / 65 of the g_u image stay zero: no halo MFMA tile
+template <bool MASKED, bool ONESEG, bool HAS_D, bool SX, bool WHOLE>
 __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
+    static_assert(!WHOLE || (ONESEG && !MASKED), "WHOLE is a one-segment layout");
     __shared__ __attribute__((aligned(16))) uint8_t XS[ISLOT];        // split tot image
     __shared__ __attribute__((aligned(16))) uint8_t XG[GROWS * RS];   // split g_u image
     __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];     // fp32 tot + D_l rows
@@ -100,7 +104,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     // to unused row 66).  Other layouts: the tile's columns, no halo rows.
     // masked layouts have the one-segment geometry (row L = position p0 + L - 1, gathered) and
     // a tile may start / end inside a sub-sequence: the same halo rows, tap masks in g_a
-    constexpr bool HALO = ONESEG || MASKED;
+    constexpr bool HALO = (ONESEG && !WHOLE) || MASKED;
     int Lv[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) Lv[j] = HALO ? Lc[j] + 1 : Lc[j];
@@ -449,13 +453,16 @@ void launch_block_bwd_s(const BwdArgsS& a0, hipStream_t s) {
     const bool masked = pick_layout(a.n, ly);
     const bool oneseg = !masked && ly.M == TMS;
     if (a.spart && (!oneseg || a.dadd || a.d != 1)) { fprintf(stderr, "block_bwd_s: spart needs d = 1, no D\n"); abort(); }
-#define BWD_LAUNCH(M, O, D, X) hipLaunchKernelGGL((k_block_bwd_s<M, O, D, X>), grid, dim3(FT), 0, s, a, ly)
-    if (masked) { if (a.dadd) BWD_LAUNCH(true, false, true, false); else BWD_LAUNCH(true, false, false, false); }
-    else if (oneseg) {
-        if (a.dadd) BWD_LAUNCH(false, true, true, false);
-        else if (a.spart) BWD_LAUNCH(false, true, false, true);
-        else BWD_LAUNCH(false, true, false, false);
-    } else { if (a.dadd) BWD_LAUNCH(false, false, true, false); else BWD_LAUNCH(false, false, false, false); }
+    const bool whole = oneseg && a.n == TMS;
+#define BWD_LAUNCH(M, O, D, X, W) hipLaunchKernelGGL((k_block_bwd_s<M, O, D, X, W>), grid, dim3(FT), 0, s, a, ly)
+    if (masked) { if (a.dadd) BWD_LAUNCH(true, false, true, false, false); else BWD_LAUNCH(true, false, false, false, false); }
+    else if (whole && !a.spart) {
+        if (a.dadd) BWD_LAUNCH(false, true, true, false, true); else BWD_LAUNCH(false, true, false, false, true);
+    } else if (oneseg) {
+        if (a.dadd) BWD_LAUNCH(false, true, true, false, false);
+        else if (a.spart) BWD_LAUNCH(false, true, false, true, false);
+        else BWD_LAUNCH(false, true, false, false, false);
+    } else { if (a.dadd) BWD_LAUNCH(false, false, true, false, false); else BWD_LAUNCH(false, false, false, false, false); }
 #undef BWD_LAUNCH
 }
 

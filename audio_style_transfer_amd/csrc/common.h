@@ -354,7 +354,8 @@ struct RangeArgs {
     const unsigned* gmax_e; const unsigned* gmax_g;   // split: [nblk + 1][B] per-clip maxima
     int split, nblk, B, T;
     float wdn[30], bdm[30], wrn[30];        // split: the per-block operand bounds (splitwave.h)
-    int* flags;                             // [B]
+    int* flags;                             // [B] OR'ed (sticky)
+    int* last;                              // [B] this evaluation's alone
 };
 void launch_range_flags(const RangeArgs& a, hipStream_t s);
 

@@ -491,6 +491,12 @@ __global__ void __launch_bounds__(256) k_zero32(uint32_t* __restrict__ p, size_t
 void launch_zero32(void* p, size_t bytes, hipStream_t s) {
     const size_t n = bytes / 4;
     if (!n) return;
+#ifdef ASTYLE_MEMSET_CLEARS
+    // tools-only build (ASTYLE_VARIANT=memset ASTYLE_DEFS=-DASTYLE_MEMSET_CLEARS): the round-4
+    // hipMemsetAsync clears, for tools/determinism2.py (graph replays)
+    (void)hipMemsetAsync(p, 0, bytes, s);
+    return;
+#endif
     const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
     hipLaunchKernelGGL(k_zero32, dim3(blocks), dim3(256), 0, s, (uint32_t*)p, n);
 }

@@ -263,6 +263,7 @@ __global__ void __launch_bounds__(256) k_range_flags(RangeArgs a) {
         }
     }
     a.flags[b] |= f;   // sticky until ast_range_flags_reset / ast_lbfgs_begin
+    a.last[b] = f;     // ast_range_flags_last: this evaluation only
 }
 
 void launch_range_flags(const RangeArgs& a, hipStream_t s) {

@@ -259,10 +259,14 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // scalar load of a uniform word: a compiler-visible vector load would make the compiler wait
-// for every older vector-memory op, the kernels' in-flight DMA included
+// for every older vector-memory op, the kernels' in-flight DMA included.  The words it reads are
+// per-clip maxima that atomics of the previous launch wrote from every XCD: glc makes the load
+// miss in the scalar cache (no stale line carried over from an earlier read of the same word),
+// so the value comes from the coherent level whatever the launch path's own cache maintenance
+// (read-only: nothing is written through the scalar cache)
 __device__ __forceinline__ float sload(const float* p) {
     float v;
-    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
     return v;
 }
 

@@ -218,6 +218,12 @@ class StyleEngine:
             self.reset_range_flags()
         return out
 
+    def range_flags_last(self) -> torch.Tensor:
+        """The same flags for the most recent loss_grad alone (ast_range_flags_last)."""
+        out = torch.empty(self.batch, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.ast_range_flags_last(self.h, self._ptr(out, torch.int32), self._stream()))
+        return out
+
     def reset_range_flags(self) -> None:
         _lib.check(self.lib.ast_range_flags_reset(self.h, self._stream()))
 

@@ -28,9 +28,21 @@ def _as_dev(a, device):
     return torch.as_tensor(np.asarray(a, dtype=np.float64), device=device).contiguous()
 
 
+MAX_CELLS = 1 << 16    # n1 * n2 per problem (ast_ot_admm)
+
+
 def ot_admm_batched(p_mod, p_ref, eps=1e-4, miter=1e5, palette=True, device=None):
     """p_mod [B, n1, d], p_ref [B, n2, d] -> (plans [B, n1, n2], palettes [B, n1, d] or None,
-    iterations [B]) as device tensors; one OT_ADMM + transform_palette per pair."""
+    iterations [B]) as device tensors; one OT_ADMM + transform_palette per pair.
+
+    Size limit: n1 * n2 <= 2^16 cells (MAX_CELLS; e.g. 256 x 256) and n1 + n2 <= 20000.  The
+    reference's OT_ADMM has no limit, but one problem runs on one workgroup whose ADMM iteration
+    streams ~80 B per cell, so 2^16 cells already take seconds per solve and 2^26 (the round-3
+    limit) would take hours; larger palettes raise ValueError here (the C ABI: AST_E_ARG)."""
+    n1, n2 = int(p_mod.shape[-2]), int(p_ref.shape[-2])
+    if n1 * n2 > MAX_CELLS or n1 + n2 > 20000:
+        raise ValueError('ot_admm_batched: %d x %d palettes exceed the solver limit n1 * n2 <= %d '
+                         '(and n1 + n2 <= 20000)' % (n1, n2, MAX_CELLS))
     lib = _lib.load()
     dev = p_mod.device if isinstance(p_mod, torch.Tensor) and p_mod.is_cuda else _dev(device)
     a = _as_dev(p_mod, dev)

@@ -107,6 +107,8 @@ int ast_loss_grad_phase(ast_ctx* ctx, const float* x_dev, float* grad_dev, float
                         int phase, void* stream);
 
 /* Per-clip flags accumulated (OR) over every ast_loss_grad since the last reset, into flags_dev
+ * (round 4 changed this from "the last call's flags" to sticky; ast_range_flags_last keeps the
+ * old per-call meaning)
  * [batch] (int, device) -- sticky, so an out-of-range line-search trial inside a device
  * L-BFGS-B epoch stays visible after the epoch (the reference's ScipyOptimizerInterface sees
  * every evaluation, methods.py:164-181).  Reset: ast_range_flags_reset, ast_lbfgs_begin with
@@ -126,6 +128,10 @@ int ast_loss_grad_phase(ast_ctx* ctx, const float* x_dev, float* grad_dev, float
 #define AST_RANGE_GRAD 4
 #define AST_RANGE_TINY 8
 int ast_range_flags(ast_ctx* ctx, int* flags_dev, void* stream);
+/* The same bits for the most recent ast_loss_grad alone (the per-call meaning ast_range_flags
+ * had before round 4: a host that checks after every evaluation and never resets can use this
+ * one).  Graph-capturable. */
+int ast_range_flags_last(ast_ctx* ctx, int* flags_dev, void* stream);
 /* Clear the accumulated range flags (stream-ordered; graph-capturable). */
 int ast_range_flags_reset(ast_ctx* ctx, void* stream);
 

@@ -213,6 +213,8 @@ def test_range_flags_cover_every_evaluation_of_a_device_epoch(weights, dev):
     assert not info[:, 0].any(), info
     f = eng.range_flags().cpu().tolist()
     assert f[0] & (1 | 2) and f[1] == 0, f
+    # the per-call getter (ast_range_flags_last) reports the epoch's last, in-range evaluation
+    assert eng.range_flags_last().cpu().tolist() == [0, 0]
     eng.reset_range_flags()
     eng.loss_grad(x64.float().contiguous())
     assert eng.range_flags().cpu().tolist() == [0, 0]

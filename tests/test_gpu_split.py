@@ -441,6 +441,21 @@ def test_loss_grad_phases_and_clip_groups(weights, dev):
     eng.loss_grad_phase(x0, g1, p1, 1)
     eng.loss_grad_phase(x0, g1, p1, 2)
     assert torch.equal(p0, p1) and torch.equal(g0, g1)
+    # between the phases the tapped tensors hold D, not activations (extracts are
+    # refused), and a forward / new targets / new gamma in between void phase 1
+    for between in (lambda: eng.forward(x0), lambda: _set(eng, 'ours', T, weights),
+                    lambda: eng.set_gamma(0.0)):
+        eng.loss_grad_phase(x0, g1, p1, 1)
+        with pytest.raises(AstError, match='ast_forward has not run'):
+            eng.extract(29)
+        between()
+        with pytest.raises(AstError, match='phase 1 first'):
+            eng.loss_grad_phase(x0, g1, p1, 2)
+    eng.loss_grad_phase(x0, g1, p1, 1)
+    eng.loss_grad_phase(x0, g1, p1, 2)
+    assert torch.equal(p0, p1) and torch.equal(g0, g1)
+    # ast_range_flags_last: the last evaluation alone; ast_range_flags: sticky since the reset
+    assert not eng.range_flags_last().any()
     loop = AdamLoop(eng, x0.clone(), lr=1.0, graph=True)
     for _ in range(3):
         loop.step()
