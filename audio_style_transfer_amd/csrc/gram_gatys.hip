@@ -14,6 +14,7 @@
 //        both operands so a lane's 8 k-steps walk one 128-B half row), C lands as 4
 //        consecutive channels per lane -> 8-B (bf16) / 16-B (fp32) stores of the same rows.
 #include "common.h"
+#include <type_traits>
 #include <cstdlib>
 
 namespace ast {
@@ -340,8 +341,11 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
     const int c4 = tid & 31, r0 = tid >> 5;
     // NST stages of loads in flight (a ring of register sets)
     float4 vr[NST][8];
+    // unconditional loads (past the chunk a stage re-reads its last block, an L2 hit) and whole
+    // rings in the loop: a conditional load made the compiler copy the ring registers behind
+    // vmcnt(0) waits, so nothing stayed in flight across a stage (the ours-Gram forward's fix)
     auto load = [&](float4 (&v)[8], int k) {
-        const float* src = E + (size_t)k * GYB * C + (size_t)r0 * C + 4 * c4;
+        const float* src = E + (size_t)min(k, nt - 1) * GYB * C + (size_t)r0 * C + 4 * c4;
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(src + (size_t)(8 * q) * C);
     };
@@ -368,42 +372,52 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
     };
-    auto stage = [&](float4 (&v)[8], int k) {
-        __syncthreads();   // the previous stage's fragment reads are done
+    // the diagonal / off-diagonal waves run separate copies of the loop (DIAG a constant in
+    // each), so the accumulators keep their registers across iterations
+    auto run = [&](auto diag_tag) {
+        constexpr bool DIAG = decltype(diag_tag)::value;
+        auto stage = [&](float4 (&v)[8], int k) {
+            __syncthreads();   // the previous stage's fragment reads are done
 #pragma unroll
-        for (int qq = 0; qq < 8; ++qq) {
-            const int r = r0 + 8 * qq;
-            uint32_t h0, l0, h1, l1;
-            split2g(v[qq].x, v[qq].y, h0, l0);
-            split2g(v[qq].z, v[qq].w, h1, l1);
-            *reinterpret_cast<uint2*>(&Lh[img(r)]) = make_uint2(h0, h1);
-            *reinterpret_cast<uint2*>(&Ll[img(r)]) = make_uint2(l0, l1);
-        }
-        if (k + NST < nt) load(v, k + NST);   // NST stages ahead
-        __syncthreads();
-#pragma unroll
-        for (int s = 0; s < GYB / 16; ++s) {
-            const bf16x8 h0 = frag(Lh, o0, s), l0 = frag(Ll, o0, s);
-            const bf16x8 h1 = frag(Lh, o1, s), l1 = frag(Ll, o1, s);
-            if (diag) {
-                mm3(acc[0], h0, l0, h0, l0);     // (X0, X0)
-                mm3(acc[1], h0, l0, h1, l1);     // (X0, X0 + 1)
-                mm3(acc[2], h1, l1, h1, l1);     // (X0 + 1, X0 + 1)
-            } else {
-                const bf16x8 h2 = frag(Lh, o2, s), l2 = frag(Ll, o2, s);
-                mm3(acc[0], h0, l0, h1, l1);     // (X0, 2)
-                mm3(acc[1], h0, l0, h2, l2);     // (X0, 3)
+            for (int qq = 0; qq < 8; ++qq) {
+                const int r = r0 + 8 * qq;
+                uint32_t h0, l0, h1, l1;
+                split2g(v[qq].x, v[qq].y, h0, l0);
+                split2g(v[qq].z, v[qq].w, h1, l1);
+                *reinterpret_cast<uint2*>(&Lh[img(r)]) = make_uint2(h0, h1);
+                *reinterpret_cast<uint2*>(&Ll[img(r)]) = make_uint2(l0, l1);
             }
+            load(v, k + NST);   // NST stages ahead
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < GYB / 16; ++s) {
+                const bf16x8 h0 = frag(Lh, o0, s), l0 = frag(Ll, o0, s);
+                const bf16x8 h1 = frag(Lh, o1, s), l1 = frag(Ll, o1, s);
+                if (DIAG) {
+                    mm3(acc[0], h0, l0, h0, l0);     // (X0, X0)
+                    mm3(acc[1], h0, l0, h1, l1);     // (X0, X0 + 1)
+                    mm3(acc[2], h1, l1, h1, l1);     // (X0 + 1, X0 + 1)
+                } else {
+                    const bf16x8 h2 = frag(Lh, o2, s), l2 = frag(Ll, o2, s);
+                    mm3(acc[0], h0, l0, h1, l1);     // (X0, 2)
+                    mm3(acc[1], h0, l0, h2, l2);     // (X0, 3)
+                }
+            }
+        };
+#pragma unroll
+        for (int q = 0; q < NST; ++q) load(vr[q], q);
+        const int nring = nt / NST;
+        int k = 0;
+        for (int i = 0; i < nring; ++i, k += NST) {
+#pragma unroll
+            for (int q = 0; q < NST; ++q) stage(vr[q], k + q);
         }
+#pragma unroll
+        for (int q = 0; q < NST - 1; ++q)
+            if (q < nt - nring * NST) stage(vr[q], k + q);
     };
-#pragma unroll
-    for (int q = 0; q < NST; ++q)
-        if (q < nt) load(vr[q], q);
-    for (int k = 0; k < nt; k += NST) {
-#pragma unroll
-        for (int q = 0; q < NST; ++q)
-            if (k + q < nt) stage(vr[q], k + q);
-    }
+    if (diag) run(std::true_type{});
+    else run(std::false_type{});
     float* G = a.gpart + (((size_t)b * a.nchunk + ch) * a.nu + u) * (C * C);
     if (diag) {
         store_tile(G, X0, X0, acc[0], lane);
@@ -428,13 +442,19 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
 // content partials -- k_content's 2 GiB gradient buffer, written and read back, is gone.
 typedef float f32x4g __attribute__((ext_vector_type(4)));
 constexpr int GB2 = 3;   // blocks in flight
+// CONT: this launch is the content tensor's (a.cont_u) alone; otherwise every other tensor
+// (two launches when a content tap is fused, so each copy of the loop is straight-line code).
+// HCG: some launched tensor also has a content-gradient buffer to add.
+template <bool CONT, bool HCG>
 __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
     __shared__ __attribute__((aligned(16))) u16 Sh[C * SBS];   // S~ hi
     __shared__ __attribute__((aligned(16))) u16 Sl[C * SBS];   // S~ lo
     const int tilesPer = a.T / GY_ROWS;
+    const int nul = CONT ? 1 : a.nu - (a.cont_u >= 0 ? 1 : 0);   // tensors of this launch
     int bid = blockIdx.x;
     const int tile = bid % tilesPer; bid /= tilesPer;
-    const int u = bid % a.nu, b = bid / a.nu;
+    const int ul = bid % nul, b = bid / nul;
+    const int u = CONT ? a.cont_u : (a.cont_u >= 0 && ul >= a.cont_u ? ul + 1 : ul);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const float* S = a.smat + ((size_t)b * a.nu + u) * (C * C);
 #pragma unroll
@@ -454,7 +474,7 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
     float* Ew = (float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;   // D (in place unless out of place)
     const float* CG = (const float*)a.cg[u];
     if (CG) CG += (size_t)b * a.T * C;
-    const bool cont = u == a.cont_u;   // (workgroup-uniform)
+    const bool cont = CONT;
     const bool top = u == a.top_u;
     float omax = 0.f;
     const float* PH = cont ? a.cont_phi + (size_t)b * a.cont_phi_bstride + a.cont_off : nullptr;
@@ -463,8 +483,11 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
     const int nblk = GY_ROWS / 4 / 16;
     const int t0 = tile * GY_ROWS + w * (GY_ROWS / 4);
     float4 vr[GB2][8];   // block in flight: k-step s, halves 0 / 1 at [2 s + hf]
+    // unconditional loads (past the tile a block re-reads the tile's last block, an L2 hit) and
+    // whole rings in the loop, the content / content-gradient work by template: a conditional
+    // load inside the loop made the compiler wait with vmcnt(0) and copy the ring registers
     auto load = [&](float4 (&v)[8], int blk) {
-        const float* src = E + (size_t)(t0 + 16 * blk + n) * C + 8 * q;
+        const float* src = E + (size_t)(t0 + 16 * min(blk, nblk - 1) + n) * C + 8 * q;
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + 32 * (k >> 1) + 4 * (k & 1));
     };
@@ -482,10 +505,9 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
             bh[s2] = make_uint4(h[0], h[1], h[2], h[3]);
             bl[s2] = make_uint4(l[0], l[1], l[2], l[3]);
         }
-        if (blk + GB2 < nblk) load(v, blk + GB2);
+        load(v, blk + GB2);
         const int t = t0 + 16 * blk + n;
         float* out = Ew + (size_t)t * C + 4 * q;
-        const float* cgr = CG ? CG + (size_t)t * C + 4 * q : nullptr;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
             f32x4g c = {0.f, 0.f, 0.f, 0.f};
@@ -499,38 +521,42 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al), __builtin_bit_cast(bf16x8, bh[s2]), c, 0, 0, 0);
             }
             float4 o4 = make_float4(c[0], c[1], c[2], c[3]);
-            if (cgr) {
-                const float4 cv = *reinterpret_cast<const float4*>(cgr + 16 * m);
+            if (HCG && CG) {
+                const float4 cv = *reinterpret_cast<const float4*>(CG + (size_t)t * C + 4 * q + 16 * m);
                 o4.x += cv.x; o4.y += cv.y; o4.z += cv.z; o4.w += cv.w;
             }
-            if (cont) {
+            if (CONT) {
                 const int cc = 16 * m + 4 * q;
-                if (cc < a.cont_ncol) {   // (phi rows hold cont_ncol channels: quads past them load nothing)
-                    const float4 ev = *reinterpret_cast<const float4*>(E + (size_t)t * C + cc);
-                    const float4 pv = *reinterpret_cast<const float4*>(PH + (size_t)t * a.cont_ncc + cc);
-                    const float d[4] = {ev.x - pv.x, ev.y - pv.y, ev.z - pv.z, ev.w - pv.w};
-                    float dd[4];
+                // phi rows hold cont_ncol (a multiple of 4) channels: quads past them read the
+                // row's last quad (in bounds) and count zero
+                const int cl = min(cc, a.cont_ncol - 4);
+                const float4 ev = *reinterpret_cast<const float4*>(E + (size_t)t * C + cc);
+                const float4 pv = *reinterpret_cast<const float4*>(PH + (size_t)t * a.cont_ncc + cl);
+                const float d[4] = {ev.x - pv.x, ev.y - pv.y, ev.z - pv.z, ev.w - pv.w};
+                float dd[4];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        dd[i] = cc + i < a.cont_ncol ? d[i] : 0.f;
-                        csd = fmaf(dd[i], dd[i], csd);
-                    }
-                    o4.x = fmaf(a.cont_coef, dd[0], o4.x); o4.y = fmaf(a.cont_coef, dd[1], o4.y);
-                    o4.z = fmaf(a.cont_coef, dd[2], o4.z); o4.w = fmaf(a.cont_coef, dd[3], o4.w);
+                for (int i = 0; i < 4; ++i) {
+                    dd[i] = cc + i < a.cont_ncol ? d[i] : 0.f;
+                    csd = fmaf(dd[i], dd[i], csd);
                 }
+                o4.x = fmaf(a.cont_coef, dd[0], o4.x); o4.y = fmaf(a.cont_coef, dd[1], o4.y);
+                o4.z = fmaf(a.cont_coef, dd[2], o4.z); o4.w = fmaf(a.cont_coef, dd[3], o4.w);
             }
             *reinterpret_cast<float4*>(out + 16 * m) = o4;
             if (top) omax = fmaxf(omax, fmaxf(fmaxf(fabsf(o4.x), fabsf(o4.y)), fmaxf(fabsf(o4.z), fabsf(o4.w))));
         }
     };
 #pragma unroll
-    for (int k = 0; k < GB2; ++k)
-        if (k < nblk) load(vr[k], k);
-    for (int blk = 0; blk < nblk; blk += GB2) {
+    for (int k = 0; k < GB2; ++k) load(vr[k], k);
+    const int nring = nblk / GB2;
+    int blk = 0;
+    for (int i = 0; i < nring; ++i, blk += GB2) {
 #pragma unroll
-        for (int k = 0; k < GB2; ++k)
-            if (blk + k < nblk) block(vr[k], blk + k);
+        for (int k = 0; k < GB2; ++k) block(vr[k], blk + k);
     }
+#pragma unroll
+    for (int k = 0; k < GB2 - 1; ++k)
+        if (k < nblk - nring * GB2) block(vr[k], blk + k);
     if (top) {    // the top tensor's max |D| per clip: one atomic per workgroup (no k_absmax pass)
         __shared__ float mw[4];
 #pragma unroll
@@ -644,7 +670,20 @@ void launch_gatys_bwd(const GatysArgs& a, int precision, hipStream_t s) {
     const dim3 g(a.B * a.nu * (a.T / GY_ROWS));
     if (precision == 1) hipLaunchKernelGGL(k_gatys_bwd_bf16, g, dim3(256), 0, s, a);
     else if (precision == 2) {
-        hipLaunchKernelGGL(k_gatys_bwd_s2, g, dim3(256), 0, s, a);
+        // the fused content tensor (if any) in a launch of its own, every other tensor in one
+        bool cg_rest = false, cg_cont = false;
+        for (int u = 0; u < a.nu; ++u) (u == a.cont_u ? cg_cont : cg_rest) |= a.cg[u] != nullptr;
+        const int nrest = a.nu - (a.cont_u >= 0 ? 1 : 0);
+        if (nrest > 0) {
+            const dim3 gr(a.B * nrest * (a.T / GY_ROWS));
+            if (cg_rest) hipLaunchKernelGGL((k_gatys_bwd_s2<false, true>), gr, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_gatys_bwd_s2<false, false>), gr, dim3(256), 0, s, a);
+        }
+        if (a.cont_u >= 0) {
+            const dim3 gc(a.B * (a.T / GY_ROWS));
+            if (cg_cont) hipLaunchKernelGGL((k_gatys_bwd_s2<true, true>), gc, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_gatys_bwd_s2<true, false>), gc, dim3(256), 0, s, a);
+        }
     }
     else hipLaunchKernelGGL(k_gatys_bwd_f32, g, dim3(256), 0, s, a);
 }

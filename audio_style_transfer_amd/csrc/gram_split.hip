@@ -90,12 +90,17 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
     for (int cc = 0; cc < 4; ++cc)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[cc][i] = 0.f;
-    // NST stages of loads in flight (a ring of NST register sets; tlen is a multiple of 2 GSS)
+    // NST stages of loads in flight (a ring of NST register sets; tlen is a multiple of 2 GSS).
+    // Every load is unconditional (past the chunk a stage re-reads the chunk's last rows, an L2
+    // hit) and the loop runs whole rings, the remainder after it: a conditional load made the
+    // compiler copy the ring registers (v_mov) behind vmcnt(0) waits, so no stage stayed in
+    // flight across a stage
     float4 v[NST][8];
     const int tend = tbeg + tlen;
     auto load = [&](float4 (&v)[8], int t0) {
+        const int tr = min(t0, tend - GSS);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(tr + k) * rs);
     };
     auto stage = [&](float4 (&v)[8], int t0) {
         uint4 fh[4], fl[4];          // channel 4 sq + j: 8 consecutive rows, hi / lo
@@ -103,7 +108,7 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
         split8<1>(v, fh[1], fl[1]);
         split8<2>(v, fh[2], fl[2]);
         split8<3>(v, fh[3], fl[3]);
-        if (t0 + NST * GSS < tend) load(v, t0 + NST * GSS);
+        load(v, t0 + NST * GSS);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -123,13 +128,16 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
         }
     };
 #pragma unroll
-    for (int q = 0; q < NST; ++q)
-        if (tbeg + q * GSS < tend) load(v[q], tbeg + q * GSS);
-    for (int t0 = tbeg; t0 < tend; t0 += NST * GSS) {
+    for (int q = 0; q < NST; ++q) load(v[q], tbeg + q * GSS);
+    const int nst = tlen / GSS, nring = nst / NST;
+    int t0 = tbeg;
+    for (int i = 0; i < nring; ++i, t0 += NST * GSS) {
 #pragma unroll
-        for (int q = 0; q < NST; ++q)
-            if (t0 + q * GSS < tend) stage(v[q], t0 + q * GSS);
+        for (int q = 0; q < NST; ++q) stage(v[q], t0 + q * GSS);
     }
+#pragma unroll
+    for (int q = 0; q < NST - 1; ++q)
+        if (q < nst - nring * NST) stage(v[q], t0 + q * GSS);
 #pragma unroll
     for (int cc = 0; cc < 4; ++cc) {
         float* dst = a.gpart + (((size_t)b * a.nchunk + ch) * C + c0 + 4 * w + cc) * 1024;
