@@ -280,7 +280,7 @@ def test_graph_replays_bitwise_at_bench_length(dev):
     clip length with 8 clips (one per XCD in the block kernels' tile order), with eager work
     between replays, and two engines' graphs interleaved.  (With hipMemsetAsync nodes for the
     per-call clears, replays after the first differed on 2 of 8 clips under the HIP runtime's
-    graph packet capture: DESIGN.md §12.)"""
+    graph packet capture: DESIGN.md §3, "Round 4: graph replays and the per-call clears".)"""
     import bench
     from audio_style_transfer_amd.engine import StyleEngine
     B, T = 8, 16384
