@@ -666,9 +666,11 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_f(GramArgs a) {
 #pragma unroll
         for (int q = 0; q < 3; ++q) acc[cc][q] = f32x4{0.f, 0.f, 0.f, 0.f};
     float4 v0[8], v1[8];
+    // unconditional loads (past the chunk: its last stage again), as k_gram_fwd_s
     auto load = [&](float4 (&v)[8], int t0) {
+        const int tr = min(t0, tbeg + tlen - GSS);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(tr + k) * rs);
     };
     auto stage = [&](float4 (&v)[8], int t0) {
         float4 f[4][2];   // channel 4 sq + j: rows 8 tb .. + 8
@@ -678,7 +680,7 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_f(GramArgs a) {
             f[j][0] = make_float4(e(0), e(1), e(2), e(3));
             f[j][1] = make_float4(e(4), e(5), e(6), e(7));
         }
-        if (t0 + 2 * GSS < tbeg + tlen) load(v, t0 + 2 * GSS);
+        load(v, t0 + 2 * GSS);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -805,6 +807,9 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_fn(GramArgs a) {
 // kernel's (O image, whole 128-B lines, in place over E, + the content grad).
 __device__ __forceinline__ int bswz(int kq, int t) { return 8 * (kq ^ (t & 3)); }
 
+// HCG: some tensor has a content-gradient buffer (a branch around a load in the store loop
+// otherwise makes the compiler drain every stage load in flight)
+template <bool HCG>
 __global__ void __launch_bounds__(GWT) k_gram_bwd_f(GramArgs a) {
     __shared__ __attribute__((aligned(16))) float IB[GCS * GSS * 32];     // [c][t][u]
     __shared__ __attribute__((aligned(16))) float O[16 * GSS * ORS];      // [u][t][c]
@@ -836,9 +841,10 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_f(GramArgs a) {
         lrs[k] = u < a.nu ? C : 0;
     }
     float4 v0[8], v1[8];
-    auto load = [&](float4 (&v)[8], int t0) {
+    auto load = [&](float4 (&v)[8], int t0) {   // (past the chunk: its last stage again)
+        const int tr = min(t0, tend - GSS);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (size_t)(t0 + st) * lrs[k]);
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (size_t)(tr + st) * lrs[k]);
     };
     auto stage = [&](float4 (&v)[8], int t0) {
         float4 f[4][2];   // channel 4 sq + j: tensors 8 uo .. + 8 at row st
@@ -848,7 +854,7 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_f(GramArgs a) {
             f[j][0] = make_float4(e(0), e(1), e(2), e(3));
             f[j][1] = make_float4(e(4), e(5), e(6), e(7));
         }
-        if (t0 + 2 * GSS < tend) load(v, t0 + 2 * GSS);
+        load(v, t0 + 2 * GSS);
         __syncthreads();   // the previous stage's image and O reads are done
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -890,8 +896,8 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_f(GramArgs a) {
                 if (u < a.nu) {
                     float4 o = *reinterpret_cast<const float4*>(&O[(ul * GSS + tt) * ORS + 4 * q]);
                     const size_t off = (size_t)a.uid[u] * a.tstride + ((size_t)b * a.T + t0 + tt) * C + c0 + 4 * q;
-                    const float* cg = (const float*)a.cg[u];
-                    if (cg) {
+                    const float* cg = HCG ? (const float*)a.cg[u] : nullptr;
+                    if (HCG && cg) {
                         const float4 g = *reinterpret_cast<const float4*>(cg + ((size_t)b * a.T + t0 + tt) * C + c0 + 4 * q);
                         o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
                     }
@@ -939,7 +945,10 @@ void launch_gram_fwd(const GramArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gram_fwd_f, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
 void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_gram_bwd_f, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+    bool has_cg = false;
+    for (int u = 0; u < a.nu; ++u) has_cg = has_cg || a.cg[u];
+    if (has_cg) hipLaunchKernelGGL(k_gram_bwd_f<true>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
+    else hipLaunchKernelGGL(k_gram_bwd_f<false>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
 static int gram_bwd_pipe() {   // ASTYLE_GRAM_BWD_PIPE=1: the two-barrier kernel (A/B)
     static int v = -1;
