@@ -442,19 +442,13 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
 // content partials -- k_content's 2 GiB gradient buffer, written and read back, is gone.
 typedef float f32x4g __attribute__((ext_vector_type(4)));
 constexpr int GB2 = 3;   // blocks in flight
-// CONT: this launch is the content tensor's (a.cont_u) alone; otherwise every other tensor
-// (two launches when a content tap is fused, so each copy of the loop is straight-line code).
-// HCG: some launched tensor also has a content-gradient buffer to add.
-template <bool CONT, bool HCG>
 __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
     __shared__ __attribute__((aligned(16))) u16 Sh[C * SBS];   // S~ hi
     __shared__ __attribute__((aligned(16))) u16 Sl[C * SBS];   // S~ lo
     const int tilesPer = a.T / GY_ROWS;
-    const int nul = CONT ? 1 : a.nu - (a.cont_u >= 0 ? 1 : 0);   // tensors of this launch
     int bid = blockIdx.x;
     const int tile = bid % tilesPer; bid /= tilesPer;
-    const int ul = bid % nul, b = bid / nul;
-    const int u = CONT ? a.cont_u : (a.cont_u >= 0 && ul >= a.cont_u ? ul + 1 : ul);
+    const int u = bid % a.nu, b = bid / a.nu;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const float* S = a.smat + ((size_t)b * a.nu + u) * (C * C);
 #pragma unroll
@@ -474,7 +468,7 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
     float* Ew = (float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C;   // D (in place unless out of place)
     const float* CG = (const float*)a.cg[u];
     if (CG) CG += (size_t)b * a.T * C;
-    const bool cont = CONT;
+    const bool cont = u == a.cont_u;   // (workgroup-uniform)
     const bool top = u == a.top_u;
     float omax = 0.f;
     const float* PH = cont ? a.cont_phi + (size_t)b * a.cont_phi_bstride + a.cont_off : nullptr;
@@ -483,11 +477,8 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
     const int nblk = GY_ROWS / 4 / 16;
     const int t0 = tile * GY_ROWS + w * (GY_ROWS / 4);
     float4 vr[GB2][8];   // block in flight: k-step s, halves 0 / 1 at [2 s + hf]
-    // unconditional loads (past the tile a block re-reads the tile's last block, an L2 hit) and
-    // whole rings in the loop, the content / content-gradient work by template: a conditional
-    // load inside the loop made the compiler wait with vmcnt(0) and copy the ring registers
     auto load = [&](float4 (&v)[8], int blk) {
-        const float* src = E + (size_t)(t0 + 16 * min(blk, nblk - 1) + n) * C + 8 * q;
+        const float* src = E + (size_t)(t0 + 16 * blk + n) * C + 8 * q;
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(src + 32 * (k >> 1) + 4 * (k & 1));
     };
@@ -505,9 +496,10 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
             bh[s2] = make_uint4(h[0], h[1], h[2], h[3]);
             bl[s2] = make_uint4(l[0], l[1], l[2], l[3]);
         }
-        load(v, blk + GB2);
+        if (blk + GB2 < nblk) load(v, blk + GB2);
         const int t = t0 + 16 * blk + n;
         float* out = Ew + (size_t)t * C + 4 * q;
+        const float* cgr = CG ? CG + (size_t)t * C + 4 * q : nullptr;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
             f32x4g c = {0.f, 0.f, 0.f, 0.f};
@@ -521,42 +513,38 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al), __builtin_bit_cast(bf16x8, bh[s2]), c, 0, 0, 0);
             }
             float4 o4 = make_float4(c[0], c[1], c[2], c[3]);
-            if (HCG && CG) {
-                const float4 cv = *reinterpret_cast<const float4*>(CG + (size_t)t * C + 4 * q + 16 * m);
+            if (cgr) {
+                const float4 cv = *reinterpret_cast<const float4*>(cgr + 16 * m);
                 o4.x += cv.x; o4.y += cv.y; o4.z += cv.z; o4.w += cv.w;
             }
-            if (CONT) {
+            if (cont) {
                 const int cc = 16 * m + 4 * q;
-                // phi rows hold cont_ncol (a multiple of 4) channels: quads past them read the
-                // row's last quad (in bounds) and count zero
-                const int cl = min(cc, a.cont_ncol - 4);
-                const float4 ev = *reinterpret_cast<const float4*>(E + (size_t)t * C + cc);
-                const float4 pv = *reinterpret_cast<const float4*>(PH + (size_t)t * a.cont_ncc + cl);
-                const float d[4] = {ev.x - pv.x, ev.y - pv.y, ev.z - pv.z, ev.w - pv.w};
-                float dd[4];
+                if (cc < a.cont_ncol) {   // (phi rows hold cont_ncol channels: quads past them load nothing)
+                    const float4 ev = *reinterpret_cast<const float4*>(E + (size_t)t * C + cc);
+                    const float4 pv = *reinterpret_cast<const float4*>(PH + (size_t)t * a.cont_ncc + cc);
+                    const float d[4] = {ev.x - pv.x, ev.y - pv.y, ev.z - pv.z, ev.w - pv.w};
+                    float dd[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    dd[i] = cc + i < a.cont_ncol ? d[i] : 0.f;
-                    csd = fmaf(dd[i], dd[i], csd);
+                    for (int i = 0; i < 4; ++i) {
+                        dd[i] = cc + i < a.cont_ncol ? d[i] : 0.f;
+                        csd = fmaf(dd[i], dd[i], csd);
+                    }
+                    o4.x = fmaf(a.cont_coef, dd[0], o4.x); o4.y = fmaf(a.cont_coef, dd[1], o4.y);
+                    o4.z = fmaf(a.cont_coef, dd[2], o4.z); o4.w = fmaf(a.cont_coef, dd[3], o4.w);
                 }
-                o4.x = fmaf(a.cont_coef, dd[0], o4.x); o4.y = fmaf(a.cont_coef, dd[1], o4.y);
-                o4.z = fmaf(a.cont_coef, dd[2], o4.z); o4.w = fmaf(a.cont_coef, dd[3], o4.w);
             }
             *reinterpret_cast<float4*>(out + 16 * m) = o4;
             if (top) omax = fmaxf(omax, fmaxf(fmaxf(fabsf(o4.x), fabsf(o4.y)), fmaxf(fabsf(o4.z), fabsf(o4.w))));
         }
     };
 #pragma unroll
-    for (int k = 0; k < GB2; ++k) load(vr[k], k);
-    const int nring = nblk / GB2;
-    int blk = 0;
-    for (int i = 0; i < nring; ++i, blk += GB2) {
+    for (int k = 0; k < GB2; ++k)
+        if (k < nblk) load(vr[k], k);
+    for (int blk = 0; blk < nblk; blk += GB2) {
 #pragma unroll
-        for (int k = 0; k < GB2; ++k) block(vr[k], blk + k);
+        for (int k = 0; k < GB2; ++k)
+            if (blk + k < nblk) block(vr[k], blk + k);
     }
-#pragma unroll
-    for (int k = 0; k < GB2 - 1; ++k)
-        if (k < nblk - nring * GB2) block(vr[k], blk + k);
     if (top) {    // the top tensor's max |D| per clip: one atomic per workgroup (no k_absmax pass)
         __shared__ float mw[4];
 #pragma unroll
@@ -670,20 +658,7 @@ void launch_gatys_bwd(const GatysArgs& a, int precision, hipStream_t s) {
     const dim3 g(a.B * a.nu * (a.T / GY_ROWS));
     if (precision == 1) hipLaunchKernelGGL(k_gatys_bwd_bf16, g, dim3(256), 0, s, a);
     else if (precision == 2) {
-        // the fused content tensor (if any) in a launch of its own, every other tensor in one
-        bool cg_rest = false, cg_cont = false;
-        for (int u = 0; u < a.nu; ++u) (u == a.cont_u ? cg_cont : cg_rest) |= a.cg[u] != nullptr;
-        const int nrest = a.nu - (a.cont_u >= 0 ? 1 : 0);
-        if (nrest > 0) {
-            const dim3 gr(a.B * nrest * (a.T / GY_ROWS));
-            if (cg_rest) hipLaunchKernelGGL((k_gatys_bwd_s2<false, true>), gr, dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((k_gatys_bwd_s2<false, false>), gr, dim3(256), 0, s, a);
-        }
-        if (a.cont_u >= 0) {
-            const dim3 gc(a.B * (a.T / GY_ROWS));
-            if (cg_cont) hipLaunchKernelGGL((k_gatys_bwd_s2<true, true>), gc, dim3(256), 0, s, a);
-            else hipLaunchKernelGGL((k_gatys_bwd_s2<true, false>), gc, dim3(256), 0, s, a);
-        }
+        hipLaunchKernelGGL(k_gatys_bwd_s2, g, dim3(256), 0, s, a);
     }
     else hipLaunchKernelGGL(k_gatys_bwd_f32, g, dim3(256), 0, s, a);
 }

@@ -33,8 +33,6 @@ constexpr int BRS = 40;       // bwd images [c][t][u] row stride (bf16): 80 B
 constexpr int ORS = 36;       // bwd output image [u][t][c] row stride (floats): 144 B
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     const int xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
@@ -222,7 +220,10 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_n(GramArgs a) {
 // CONT: the fused content tap (a.cont_u >= 0); false: the round-2 kernel.  NST stages of loads
 // in flight: 2 (the split of a stage into registers before the barrier) or 3 (each channel split
 // straight into the image after the barrier: 24 fewer live registers pay for the third stage)
-template <bool CONT, int NST>
+// HCG: some tensor has a content-gradient buffer to add (not the fused configs): without it
+// the store loop has no branch around a load (a load there made the compiler drain every stage
+// load in flight with vmcnt(0))
+template <bool CONT, int NST, bool HCG>
 __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     __shared__ __attribute__((aligned(16))) u16 IH[GCS * GSS * BRS];       // [c][t][u] hi
     __shared__ __attribute__((aligned(16))) u16 IL[GCS * GSS * BRS];       // [c][t][u] lo
@@ -277,9 +278,12 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     const float* cp_src = CONT ? a.cont_phi + (size_t)b * a.cont_phi_bstride + a.cont_off + c0 + 4 * cq : nullptr;
     // NST stages of loads in flight (a ring of register sets; tlen is a multiple of 2 GSS)
     float4 vr[NST][8];
+    // unconditional loads (past the chunk a stage re-reads the chunk's last stage, an L2 hit):
+    // a conditional load made the compiler copy the ring registers behind vmcnt(0) waits
     auto load = [&](float4 (&v)[8], int t0) {
+        const int tr = min(t0, tend - GSS);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (lrs[k] ? lofs + (uint32_t)(t0 + st) * C : 0u));
+        for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(ld[k] + (lrs[k] ? lofs + (uint32_t)(tr + st) * C : 0u));
     };
     auto stage = [&](float4 (&v)[8], int t0) {
         float4 ce, cph = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -296,7 +300,7 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
             split8<1>(v, fh[1], fl[1]);
             split8<2>(v, fh[2], fl[2]);
             split8<3>(v, fh[3], fl[3]);
-            if (t0 + NST * GSS < tend) load(v, t0 + NST * GSS);
+            load(v, t0 + NST * GSS);
             __syncthreads();   // the previous stage's image and O reads are done
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -311,7 +315,7 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
                        *reinterpret_cast<uint4*>(&IH[o]) = fh; *reinterpret_cast<uint4*>(&IL[o]) = fl; }
             SPLIT_ONE(0) SPLIT_ONE(1) SPLIT_ONE(2) SPLIT_ONE(3)
 #undef SPLIT_ONE
-            if (t0 + NST * GSS < tend) load(v, t0 + NST * GSS);
+            load(v, t0 + NST * GSS);
         }
         __syncthreads();
         // D_c = S~_c E_c of column half m for the wave's 4 channels (the B fragments re-read per
@@ -365,8 +369,8 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
                 if (u < a.nu) {
                     float4 o = *reinterpret_cast<const float4*>(&O[(ul * GSS + tt) * ORS + 4 * q]);
                     const size_t off = (size_t)a.uid[u] * a.tstride + ((size_t)b * a.T + t0 + tt) * C + c0 + 4 * q;
-                    const float* cg = (const float*)a.cg[u];
-                    if (cg) {
+                    const float* cg = HCG ? (const float*)a.cg[u] : nullptr;
+                    if (HCG && cg) {
                         const float4 g = *reinterpret_cast<const float4*>(cg + ((size_t)b * a.T + t0 + tt) * C + c0 + 4 * q);
                         o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
                     }
@@ -396,238 +400,23 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
         }
         csd = 0.f;
     };
-    for (int t0 = tbeg; t0 < tend; t0 += NST * GSS) {
+    const int nring = (tlen / GSS) / NST;
+    int t0 = tbeg;
+    for (int i = 0; i < nring; ++i, t0 += NST * GSS) {
 #pragma unroll
-        for (int q = 0; q < NST; ++q)
-            if (t0 + q * GSS < tend) {
-                stage(vr[q], t0 + q * GSS);
-                if (CONT && (t0 + (q + 1) * GSS) % GRAM_CSLOT == 0) flush_c((t0 + q * GSS) / GRAM_CSLOT);
-            }
+        for (int q = 0; q < NST; ++q) {
+            stage(vr[q], t0 + q * GSS);
+            if (CONT && (t0 + (q + 1) * GSS) % GRAM_CSLOT == 0) flush_c((t0 + q * GSS) / GRAM_CSLOT);
+        }
     }
+#pragma unroll
+    for (int q = 0; q < NST - 1; ++q)
+        if (t0 + q * GSS < tend) {
+            stage(vr[q], t0 + q * GSS);
+            if (CONT && (t0 + (q + 1) * GSS) % GRAM_CSLOT == 0) flush_c((t0 + q * GSS) / GRAM_CSLOT);
+        }
     if (a.top_u >= 0) {   // one atomic per workgroup
         __shared__ float wm[GWT / 64];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) omax = fmaxf(omax, __shfl_xor(omax, off));
-        if (lane == 0) wm[w] = omax;
-        __syncthreads();
-        if (tid == 0) {
-            float m = wm[0];
-#pragma unroll
-            for (int k = 1; k < GWT / 64; ++k) m = fmaxf(m, wm[k]);
-            atomicMax(a.gmax_top + b, __float_as_uint(m));
-        }
-    }
-}
-
-// backward, pipelined (k_gram_bwd_p): the same work as k_gram_bwd_s with two barriers per
-// stage instead of five.  Both column halves' D go to an O image of their own (2 x 36 KiB; with
-// the split images 152 KiB of LDS), so one barrier separates "images hold stage t, O free" from
-// "O holds stage t, images free": after it every wave stores stage t from O and writes stage
-// t + 1's split rows into the images, and the next barrier closes both.  The steady-state body
-// has no branch around a vector-memory instruction (the compiler's vmcnt accounting merges
-// paths conservatively, and a wait on a young load drains every older one): future-stage loads
-// are unconditional (past the chunk they re-read its last stage, an L2 hit); stores go through
-// a per-tensor buffer resource whose range is 0 for the padding tensors (u >= nu: dropped by
-// the hardware); the content tap's E / phi rows are loaded one stage ahead by every thread
-// (column offsets clamped into phi's row) and used where the wave owns them; the per-slot
-// content errors collect in LDS and leave after the loop.  HAS_CG: some tensor also has a
-// content-gradient buffer to add (not the fused configs).
-constexpr int GRAM_MAX_SLOTS = 64;   // content slots per chunk (tlen / GRAM_CSLOT)
-template <bool CONT, bool HAS_CG>
-__global__ void __launch_bounds__(GWT) k_gram_bwd_p(GramArgs a) {
-    __shared__ __attribute__((aligned(16))) u16 IH[GCS * GSS * BRS];       // [c][t][u] hi
-    __shared__ __attribute__((aligned(16))) u16 IL[GCS * GSS * BRS];       // [c][t][u] lo
-    __shared__ __attribute__((aligned(16))) float O[2 * 16 * GSS * ORS];   // [m][u][t][c]
-    __shared__ float cws[CONT ? GRAM_MAX_SLOTS * (GWT / 64) : 1];
-    __shared__ float wm[GWT / 64];
-    int b, ch, c0;
-    decode(a, b, ch, c0);
-    const int tlen = a.T / a.nchunk, tbeg = ch * tlen, tend = tbeg + tlen;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    float omax = 0.f;
-    float csd = 0.f;
-    const int i16 = lane & 15, kq = lane >> 4;
-    uint4 sa[4][2][2];
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc)
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            const float* sm = a.smat + ((size_t)b * C + c0 + 4 * w + cc) * 1024 + (16 * m + i16) * 32 + 8 * kq;
-            const float4 p = *reinterpret_cast<const float4*>(sm);
-            const float4 q = *reinterpret_cast<const float4*>(sm + 4);
-            uint32_t h[4], l[4];
-            split2(p.x, p.y, h[0], l[0]);
-            split2(p.z, p.w, h[1], l[1]);
-            split2(q.x, q.y, h[2], l[2]);
-            split2(q.z, q.w, h[3], l[3]);
-            sa[cc][m][0] = make_uint4(h[0], h[1], h[2], h[3]);
-            sa[cc][m][1] = make_uint4(l[0], l[1], l[2], l[3]);
-        }
-    const int uo = w & 3, sq = lane >> 3, st = 8 * (w >> 2) + (lane & 7);
-    // staging loads through one buffer resource per tensor (wave-uniform: scalar registers;
-    // range 0 for the padding tensors, which then read zeros) and one lane offset for all eight
-    rsrc_t lr[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int u = 8 * uo + k;
-        const bool real = u < a.nu;
-        lr[k] = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float*>((const float*)a.act + (real ? (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C : 0)),
-            (short)0, real ? 0x7fffffff : 0, 0x00020000);
-    }
-    const uint32_t lofs = (uint32_t)((c0 + 4 * sq + st * C) * 4);
-    // store pieces: tensor 16 m + 4 it + (w >> 1) (wave-uniform), row tt, quad q
-    const int tt = (tid >> 3) & 15, q = tid & 7;
-    // the fused content tap: tensor cont_u's pieces are those of the waves with (w >> 1) ==
-    // (cont_u & 3) in store iteration (cont_u & 15) >> 2 of half cont_u >> 4; those waves load
-    // its E / phi rows (the other waves' resources have range 0: zeros, no branch)
-    const int cu = a.cont_u & 31;
-    const bool cwave = CONT && (w >> 1) == (cu & 3);
-    const int cqe = CONT ? min(c0 + 4 * q, a.cont_ncol - 4) : 0;   // in phi's row (cont_ncol >= 4)
-    const rsrc_t rce = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>((const float*)a.act + (CONT ? (size_t)a.uid[cu] * a.tstride + (size_t)b * a.T * C : 0)),
-        (short)0, cwave ? 0x7fffffff : 0, 0x00020000);
-    const rsrc_t rcp = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(CONT ? a.cont_phi + (size_t)b * a.cont_phi_bstride + a.cont_off : (const float*)a.zero16),
-        (short)0, cwave ? 0x7fffffff : 0, 0x00020000);
-    const uint32_t ceo = (uint32_t)((c0 + 4 * q + tt * C) * 4);
-    const uint32_t cpo = CONT ? (uint32_t)((cqe + tt * a.cont_ncc) * 4) : 0u;
-    float4 vr[2][8];
-    auto load = [&](float4 (&v)[8], int t0) {
-        const uint32_t so = (uint32_t)(min(t0, tend - GSS) * C * 4);   // past the chunk: its last stage again
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            v[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(lr[k], lofs, so, 0));
-    };
-    auto put = [&](float4 (&v)[8]) {
-        uint4 fh, fl;
-#define SPLIT_PUT(J) { split8<J>(v, fh, fl); const int o = ((4 * sq + J) * GSS + st) * BRS + 8 * uo; \
-                       *reinterpret_cast<uint4*>(&IH[o]) = fh; *reinterpret_cast<uint4*>(&IL[o]) = fl; }
-        SPLIT_PUT(0) SPLIT_PUT(1) SPLIT_PUT(2) SPLIT_PUT(3)
-#undef SPLIT_PUT
-    };
-    float4 ce = make_float4(0.f, 0.f, 0.f, 0.f), cph = ce;   // the next stage's content rows
-    auto cload = [&](int t0) {
-        if (CONT) {
-            const int tr = min(t0, tend - GSS);
-            ce = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rce, ceo, (uint32_t)(tr * C * 4), 0));
-            cph = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rcp, cpo, (uint32_t)(tr * a.cont_ncc * 4), 0));
-        }
-    };
-    auto dhalf = [&](int m, int cc) {
-        const int o = ((4 * w + cc) * GSS + i16) * BRS + 8 * kq;
-        const uint4 bh = *reinterpret_cast<const uint4*>(&IH[o]);
-        const uint4 bl = *reinterpret_cast<const uint4*>(&IL[o]);
-        f32x4 c = {0.f, 0.f, 0.f, 0.f};
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][0]),
-                                                   __builtin_bit_cast(bf16x8, bh), c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][1]),
-                                                   __builtin_bit_cast(bf16x8, bh), c, 0, 0, 0);
-        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][0]),
-                                                      __builtin_bit_cast(bf16x8, bl), c, 0, 0, 0);
-    };
-    const float* cgb = nullptr;   // (HAS_CG: the tensor's content-gradient buffer, per piece)
-    // body of stage t0 (images hold it, O is free); vn holds stage t0 + GSS
-    auto body = [&](float4 (&vn)[8], int t0) {
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            f32x4 acc[4];
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) acc[cc] = dhalf(m, cc);
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc)
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    O[((m * 16 + 4 * kq + i) * GSS + i16) * ORS + 4 * w + cc] = acc[cc][i];
-            __builtin_amdgcn_sched_barrier(0);   // one half's accumulators and B fragments live
-        }
-        __syncthreads();   // O holds stage t0; every wave is done with the images
-        float4 cadd = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (CONT) {        // stage t0's content rows (loaded one stage ahead); used by cwave waves
-            const int cc = c0 + 4 * q;
-            const float ev[4] = {ce.x, ce.y, ce.z, ce.w}, pv[4] = {cph.x, cph.y, cph.z, cph.w};
-            float d[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                d[i] = (cwave && cc + i < a.cont_ncol) ? ev[i] - pv[i] : 0.f;
-                csd = fmaf(d[i], d[i], csd);
-            }
-            cadd = make_float4(a.cont_coef * d[0], a.cont_coef * d[1], a.cont_coef * d[2], a.cont_coef * d[3]);
-        }
-        put(vn);                           // stage t0 + GSS -> images (past the chunk: unused)
-        cload(t0 + GSS);
-        load(vn, t0 + 3 * GSS);
-        const uint32_t voff = (uint32_t)((((t0 + tt) * C) + c0 + 4 * q) * 4);
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int it = 0; it < 4; ++it) {
-                const int u = 16 * m + 4 * it + (w >> 1);
-                const bool real = u < a.nu;
-                float4 o = *reinterpret_cast<const float4*>(&O[((m * 16 + 4 * it + (w >> 1)) * GSS + tt) * ORS + 4 * q]);
-                if (HAS_CG) {
-                    cgb = real ? (const float*)a.cg[u] : nullptr;
-                    if (cgb) {
-                        const float4 g = *reinterpret_cast<const float4*>(cgb + ((size_t)b * a.T + t0 + tt) * C + c0 + 4 * q);
-                        o.x += g.x; o.y += g.y; o.z += g.z; o.w += g.w;
-                    }
-                }
-                if (CONT) {
-                    const float f = u == cu ? 1.f : 0.f;
-                    o.x = fmaf(f, cadd.x, o.x); o.y = fmaf(f, cadd.y, o.y);
-                    o.z = fmaf(f, cadd.z, o.z); o.w = fmaf(f, cadd.w, o.w);
-                }
-                const float* base = (const float*)a.actw + (real ? (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C : 0);
-                const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0,
-                                                                    real ? 0x7fffffff : 0, 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, voff, 0, 0);
-                const float mx = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
-                omax = fmaxf(omax, u == a.top_u ? mx : 0.f);
-            }
-        __syncthreads();   // the images hold stage t0 + GSS; O is free
-    };
-    // prologue: stages 0 and 1 in flight, stage 0 into the images, stage 2 loading
-    load(vr[0], tbeg);
-    load(vr[1], tbeg + GSS);
-    cload(tbeg);
-    put(vr[0]);
-    load(vr[0], tbeg + 2 * GSS);
-    __syncthreads();
-    // content errors of a finished GRAM_CSLOT-row slot -> LDS (no vector-memory op: the bodies'
-    // load accounting stays exact)
-    auto slot_done = [&](int t0) {
-        if (CONT && (t0 + GSS) % GRAM_CSLOT == 0) {
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) csd += __shfl_xor(csd, off);
-            if (lane == 0) cws[((t0 - tbeg) / GRAM_CSLOT) * (GWT / 64) + w] = csd;
-            csd = 0.f;
-        }
-    };
-    // the first body is peeled: the loop then starts with every stage load two bodies old, so
-    // the compiler's merged wait counts at the loop header stay deep (tlen: a multiple of 2 GSS)
-    body(vr[1], tbeg);
-    slot_done(tbeg);
-    int t0 = tbeg + GSS;
-    for (; t0 + GSS < tend; t0 += 2 * GSS) {
-        body(vr[0], t0);
-        slot_done(t0);
-        body(vr[1], t0 + GSS);
-        slot_done(t0 + GSS);
-    }
-    body(vr[0], t0);
-    slot_done(t0);
-    if (CONT) {   // per slot: waves 0..7 in order (batch-invariant, as k_gram_bwd_s's flush)
-        __syncthreads();
-        const int nsl = tlen / GRAM_CSLOT;
-        if (tid < nsl) {
-            float v = 0.f;
-#pragma unroll
-            for (int k = 0; k < GWT / 64; ++k) v += cws[tid * (GWT / 64) + k];
-            a.cont_part[(size_t)b * a.cont_pstride + (tbeg / GRAM_CSLOT + tid) * (C / GCS) + c0 / GCS] = v;
-        }
-    }
-    if (a.top_u >= 0) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) omax = fmaxf(omax, __shfl_xor(omax, off));
         if (lane == 0) wm[w] = omax;
@@ -950,40 +739,22 @@ void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
     if (has_cg) hipLaunchKernelGGL(k_gram_bwd_f<true>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
     else hipLaunchKernelGGL(k_gram_bwd_f<false>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
-static int gram_bwd_pipe() {   // ASTYLE_GRAM_BWD_PIPE=1: the two-barrier kernel (A/B)
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("ASTYLE_GRAM_BWD_PIPE"); v = e ? atoi(e) : 0; }
-    return v;
-}
 void launch_gram_bwd_s(const GramArgs& a, hipStream_t s) {
     const dim3 grid(a.B * a.nchunk * (C / GCS));
     if (a.cont_u >= 0 && (a.T / a.nchunk) % GRAM_CSLOT) {
         fprintf(stderr, "gram_bwd_s: the fused content tap needs whole %d-row chunks\n", GRAM_CSLOT);
         abort();
     }
-    if (gram_bwd_pipe()) {
-        bool has_cg = false;
-        for (int u = 0; u < a.nu; ++u) has_cg = has_cg || a.cg[u];
-        if ((a.T / a.nchunk) % (2 * GSS) || (a.cont_u >= 0 && ((a.T / a.nchunk) / GRAM_CSLOT > GRAM_MAX_SLOTS || a.cont_ncol < 4))) {
-            fprintf(stderr, "gram_bwd_s: chunk of %d rows / content columns %d not supported by the pipelined kernel\n", a.T / a.nchunk, a.cont_ncol);
-            abort();
-        }
-        if (a.cont_u >= 0) {
-            if (has_cg) hipLaunchKernelGGL((k_gram_bwd_p<true, true>), grid, dim3(GWT), 0, s, a);
-            else hipLaunchKernelGGL((k_gram_bwd_p<true, false>), grid, dim3(GWT), 0, s, a);
-        } else {
-            if (has_cg) hipLaunchKernelGGL((k_gram_bwd_p<false, true>), grid, dim3(GWT), 0, s, a);
-            else hipLaunchKernelGGL((k_gram_bwd_p<false, false>), grid, dim3(GWT), 0, s, a);
-        }
-        return;
-    }
+    bool has_cg = false;
+    for (int u = 0; u < a.nu; ++u) has_cg = has_cg || a.cg[u];
+#define GBS(CT, NS) if (has_cg) hipLaunchKernelGGL((k_gram_bwd_s<CT, NS, true>), grid, dim3(GWT), 0, s, a); \
+                    else hipLaunchKernelGGL((k_gram_bwd_s<CT, NS, false>), grid, dim3(GWT), 0, s, a);
     if (gram_bwd_stages() == 3) {
-        if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 3>), grid, dim3(GWT), 0, s, a);
-        else hipLaunchKernelGGL((k_gram_bwd_s<false, 3>), grid, dim3(GWT), 0, s, a);
+        if (a.cont_u >= 0) { GBS(true, 3) } else { GBS(false, 3) }
     } else {
-        if (a.cont_u >= 0) hipLaunchKernelGGL((k_gram_bwd_s<true, 2>), grid, dim3(GWT), 0, s, a);
-        else hipLaunchKernelGGL((k_gram_bwd_s<false, 2>), grid, dim3(GWT), 0, s, a);
+        if (a.cont_u >= 0) { GBS(true, 2) } else { GBS(false, 2) }
     }
+#undef GBS
 }
 
 }  // namespace ast
