@@ -260,13 +260,15 @@ __device__ __forceinline__ void lds_barrier() {
 
 // scalar load of a uniform word: a compiler-visible vector load would make the compiler wait
 // for every older vector-memory op, the kernels' in-flight DMA included.  The words it reads are
-// per-clip maxima that atomics of the previous launch wrote from every XCD: glc makes the load
-// miss in the scalar cache (no stale line carried over from an earlier read of the same word),
-// so the value comes from the coherent level whatever the launch path's own cache maintenance
-// (read-only: nothing is written through the scalar cache)
+// per-clip maxima that atomics of the PREVIOUS launch on the same stream wrote: the kernel
+// boundary (the producer's end-of-kernel release, this kernel's start acquire, which invalidates
+// the scalar cache) makes them visible.  Round 5 measured the glc form (a miss in the scalar
+// cache on every load): no change to the graph-replay defect of DESIGN.md §3, and +1.3 ms per
+// step at one clip, where every workgroup of a launch reads the same word (configs[1]: 478 ->
+// 299 iters/s); reverted
 __device__ __forceinline__ float sload(const float* p) {
     float v;
-    asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
     return v;
 }
 

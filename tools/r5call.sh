@@ -1,4 +1,6 @@
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_parity.py tests/test_gpu_precision.py -x -q --timeout 200 --timeout-method thread > gpurun_out/split_default.log 2>&1 || { tail -30 gpurun_out/split_default.log; exit 1; }
-tail -2 gpurun_out/split_default.log
-bash tools/r5ab.sh "base|ASTYLE_LIB=audio_style_transfer_amd/libastyle_base.so|" "cur||" "base_g|ASTYLE_LIB=audio_style_transfer_amd/libastyle_base.so|--gatys" "cur_g||--gatys" "base_b|ASTYLE_LIB=audio_style_transfer_amd/libastyle_base.so|" "cur_b||" "r4_g||--gatys" "cur_g2||--gatys"
+for v in base cur base2 cur2; do
+  case $v in base*) L=audio_style_transfer_amd/libastyle_base.so;; *) L=audio_style_transfer_amd/libastyle.so;; esac
+  ASTYLE_LIB=$L timeout -k 10 200 python bench.py --clips 1 --steps 60 --warmup 3 --side-steps 0 --cpu-baseline-seconds 0 > gpurun_out/c1_$v.log 2>&1 || { tail -20 gpurun_out/c1_$v.log; exit 1; }
+  python -c "import json; d=json.loads(open('gpurun_out/c1_$v.log').read().strip().splitlines()[-1]); k=d['kernels_ms_per_step']; print('$v', round(d['value']*256,1), 'clip-iters/s', round(d['ms_per_step'],3), 'ms', {a: round(b,3) for a,b in k.items()})"
+done
