@@ -22,7 +22,11 @@
 //   H  (one-segment layouts, unless the workgroup's previous tile is the left neighbour: then
 //      its g_u rows 64 / 65 are copied to rows 0 / 1) g_v of rows 0 / 1 (positions p0 - 1, p0;
 //      the column tiles cover p0 + 1 .. p0 + 64); carries g_u of half 1; g_u of the last column
-//      tile; barrier (g_u image complete, tot image free)
+//      tile; barrier (g_u image complete, tot image free).  The left neighbour includes the
+//      last tile of the previous sub-sequence (CARRY): that tile's right-halo column (p0 + 64,
+//      SAME padding for its own g_a) is computed on the next sub-sequence's first position
+//      instead of a zero row and set aside in g_u row 67, so the next tile's rows 0 / 1 are
+//      (0, row 67) and no tile of a walk pays the halo MFMAs but its first
 //   C  g_a, column half 0 (3 taps x 8 k-steps x 3 products over the g_u image); carries the
 //      conversion of tile i+1 and, unit by unit behind it, the row loads of tile i+2
 //   D  g_a, column half 1; carries epilogue half 0 of tile i
@@ -105,6 +109,10 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     // masked layouts have the one-segment geometry (row L = position p0 + L - 1, gathered) and
     // a tile may start / end inside a sub-sequence: the same halo rows, tap masks in g_a
     constexpr bool HALO = (ONESEG && !WHOLE) || MASKED;
+    // CARRY tiles: the last tile of a sub-sequence with a next position in the clip (p0 + 64,
+    // the next sub-sequence's first position, time q + 1)
+    constexpr bool CARRY = ONESEG && !WHOLE && !MASKED;
+    auto carry_of = [&](const Tile& t) { return CARRY && t.m0 + TMS >= a.n && t.p0 + TMS < a.T; };
     int Lv[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) Lv[j] = HALO ? Lc[j] + 1 : Lc[j];
@@ -127,6 +135,16 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         if (MASKED) {
             lt[k] = ru.load(a.tin, t, k, a.T, a.fn, a.d);
             if (HAS_D) lg[k] = ru.load(a.dadd, t, k, a.T, a.fn, a.d);
+        } else if (CARRY && k == NU - 1) {
+            // unit 8 by 64-bit address: in a CARRY tile the lanes of row 65 (lr == 1) read the
+            // next sub-sequence's first tot row (its D row stays the dummy: row 65's residual is
+            // no output)
+            const int q = t.tb - t.m0 * a.d;
+            const float* pn = a.tin + ((size_t)t.b * a.T + q + 1) * C + ru.cq;
+            const float* pr = reinterpret_cast<const float*>(
+                reinterpret_cast<const char*>(a.tin + ((ptrdiff_t)t.b * a.T + t.tb - a.d) * C) + ru.unit_off(t, k, a.fn));
+            lt[k] = *reinterpret_cast<const float4*>(carry_of(t) && ru.lr == 1 ? pn : pr);
+            if (HAS_D) lg[k] = ru.loadb(rs_d, t, k, a.fn);
         } else {
             lt[k] = ru.loadb(rs_t, t, k, a.fn);
             if (HAS_D) lg[k] = ru.loadb(rs_d, t, k, a.fn);
@@ -144,6 +162,12 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         uint8_t* p = XS + ru.imgo + 8 * k * RS;
         *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
         *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
+    };
+    // zero bits of a tile's units: a CARRY tile's row 65 is real
+    auto zbits = [&](const Tile& t) {
+        uint32_t z = ru.zero_bits(t, a.fn);
+        if (carry_of(t) && ru.lr == 1) z &= ~(1u << (NU - 1));
+        return z;
     };
     // ---- relu-mask words (u16, position-indexed): u > 0 of the tile's columns and halos,
     //      e_l > 0 of its columns ----
@@ -192,6 +216,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     };
     // g_u unit (J, g) in two parts: mask; scale + split -> image row
     float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
+    int Lv1t = Lv[1];   // row of column tile 1 (a CARRY tile: its right-halo lane r == 31 -> row 67)
     auto gu_part = [&](int J, int g, int part, float f) {
         if (part == 0) {
             const uint32_t wd_ = J < 2 ? mu_c[J] : muh_c;
@@ -205,7 +230,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
             uint32_t h01, l01, h23, l23;
             split2s(gq.x * f, gq.y * f, h01, l01);
             split2s(gq.z * f, gq.w * f, h23, l23);
-            uint8_t* p = XG + (J < 2 ? Lv[J] : Lhw) * RS + 2 * (chb + 8 * g);
+            uint8_t* p = XG + (J == 0 ? Lv[0] : J == 1 ? Lv1t : Lhw) * RS + 2 * (chb + 8 * g);
             *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
             *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
         }
@@ -310,7 +335,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
 #pragma unroll
         for (int k = 0; k < NU; ++k) load_unit(t0, k);
         load_masks(t0, mu_c, muh_c, me_c);
-        const uint32_t z0 = ru.zero_bits(t0, a.fn);
+        const uint32_t z0 = zbits(t0);
         gm_c = sload(a.gmax_in + t0.b);
         const float s0 = exp2i(scale_exp(gm_c));
 #pragma unroll
@@ -339,15 +364,21 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         const float inv2 = exp2i(-(m_u + a.kd));
         if (nt.b != cu.b) gm_c = sload(a.gmax_in + nt.b);   // (usually the same clip: tile order)
         const float s_next = exp2i(scale_exp(gm_c));
-        const uint32_t zn = ru.zero_bits(nt, a.fn);
+        const uint32_t zn = zbits(nt);
         uint8_t* erc = &ER[it & 1][0];          // this tile's residual
         uint8_t* ero = &ER[(it & 1) ^ 1][0];    // the previous tile's, then the next tile's
 
         // rows 0 / 1 from the previous tile's rows 64 / 65 when it is the left neighbour (every
         // wave its channel quarter; the previous tile's g_a reads are behind the T barrier, this
         // tile's first writes to rows 64 / 65 come in B)
-        const bool cont = HALO && !FIRST && prv.b == cu.b && prv.p0 + TMS == cu.p0 && (MASKED || cu.m0 != 0);
+        // (CARRY: the previous sub-sequence's last tile left row 65 zero and the first position's
+        // g_u in row 67: rows 0 / 1 = 0 / row 67)
+        const bool cont = HALO && !FIRST && prv.b == cu.b && prv.p0 + TMS == cu.p0 && (MASKED || CARRY || cu.m0 != 0);
+        const bool fos = CARRY && cu.m0 == 0;
+        const bool cry = carry_of(cu);
+        Lv1t = cry && r == 31 ? GROWS - 1 : Lv[1];
         const int cpo = ((lane >> 2) & 1) * 256 + 64 * w + 16 * (lane & 3);   // (side work of A)
+        const int csr = fos ? ((lane >> 3) ? GROWS - 1 : TMS) : TMS + (lane >> 3);
         uint4 cpv = make_uint4(0, 0, 0, 0);
         STAMP(11)
         // A: g_v half 0 + epilogue half 1 of the previous tile (parts 0..7)
@@ -355,9 +386,14 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
         gemm1(J0{}, [&](int kb) {
             if (!FIRST) epi_part(1, kb / 3, kb % 3, ero, me_p, inv2p);
             if (cont && lane < 16) {   // rows 64 / 65 -> 0 / 1, read one step before the write
-                if (kb == 0) cpv = lds16(XG + (TMS + (lane >> 3)) * RS + cpo);
+                if (kb == 0) {
+                    cpv = lds16(XG + csr * RS + cpo);
+                    if (fos && lane < 8) cpv = make_uint4(0, 0, 0, 0);
+                }
                 if (kb == 1) *reinterpret_cast<uint4*>(XG + (lane >> 3) * RS + cpo) = cpv;
             }
+            // a CARRY tile's row 65 is SAME padding for its own g_a (after the copy's read)
+            if (cry && lane < 8 && kb == 2) *reinterpret_cast<uint4*>(XG + (TMS + 1) * RS + cpo) = make_uint4(0, 0, 0, 0);
         });
         // B: g_v half 1 + the epilogue's parts 8..11 + g_u of half 0
         gemm1(J1{}, [&](int kb) {

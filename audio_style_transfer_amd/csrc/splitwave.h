@@ -185,11 +185,14 @@ struct RowUnits {
     __device__ __forceinline__ rsrc_t rsrc_of(const float* src, const Tile& t, int T, int d) const {
         return mk_rsrc(src + ((ptrdiff_t)t.b * T + t.tb - d) * C);
     }
-    __device__ __forceinline__ float4 loadb(rsrc_t rs, const Tile& t, int k, const FDiv& fn) const {
+    __device__ __forceinline__ uint32_t unit_off(const Tile& t, int k, const FDiv& fn) const {
         uint32_t o = soff[k];
         if (ONESEG && k == 0 && lr == 0 && t.m0 == 0) o = row1;
         if (ONESEG && k == NU - 1 && lr == 1 && t.m0 + TMS >= (int)fn.n) o = row64;
-        return bld4(rs, o, 0u);
+        return o;
+    }
+    __device__ __forceinline__ float4 loadb(rsrc_t rs, const Tile& t, int k, const FDiv& fn) const {
+        return bld4(rs, unit_off(t, k, fn), 0u);
     }
     __device__ __forceinline__ uint32_t zero_bits(const Tile& t, const FDiv& fn) const {
         uint32_t z = padz;

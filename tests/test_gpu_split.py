@@ -202,7 +202,10 @@ def test_odd_lengths_match_oracle(T, tag, precision, weights, dev):
 def test_bench_size_batch(tag, precision, weights, dev):
     """configs[2] (ours) and configs[4] (--gatys) at their size: B = 256 clips of T = 16384.
     Four clip slots (first, last, two inside) are bit-identical to a B = 1 run of the same
-    clip, and one matches the oracle."""
+    clip, and one matches the oracle.  At B = 256 every block-kernel workgroup walks one clip's
+    tiles in order, so the split backward takes its rows 0 / 1 from the previous tile (CARRY
+    rows across sub-sequences included, block_bwd_split.hip); at B = 1 each workgroup runs one
+    tile and computes them with the halo MFMA tile: the bit-identity holds the two paths equal."""
     B, T = 256, 16384
     kw = dict(CASES[tag], cont_ids=[29])
     phi_c, phi_s = O.targets_from_audio(weights, O.mu_law_numpy(synthetic_clips(1, T, 1000)[0]),
