@@ -354,8 +354,8 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
     if (x->split) {
         launch_zero32(x->gmax_e, (size_t)(NBLK_MAX + 1) * c.batch * 4, s);
         // e_0 is not stored: block 0 recomputes it from x (FwdArgsS::xin); masks and max only
-        launch_startconv_fwd((const float*)xd, (float*)nullptr, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s,
-                             (uint16_t*)x->me, x->gmax_e);
+        launch_startconv_masks((const float*)xd, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s,
+                               (uint16_t*)x->me, x->gmax_e);
     } else if (x->bf) launch_startconv_fwd((const float*)xd, (u16*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s, (uint16_t*)x->me);
     else launch_startconv_fwd((const float*)xd, (float*)x->act, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s);
     if (mark) tmark(x, s);

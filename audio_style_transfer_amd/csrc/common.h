@@ -310,6 +310,9 @@ template <typename S>
 void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b0,
                           int B, int T, hipStream_t s, uint16_t* me0 = nullptr,
                           unsigned* gmax = nullptr);
+// split mode: only the e_0 > 0 words and the per-clip max |e_0| (block 0 recomputes e_0)
+void launch_startconv_masks(const float* x, const float* w0, const float* b0, int B, int T,
+                            hipStream_t s, uint16_t* me0, unsigned* gmax);
 void launch_startx_gx(const float* spart, float* gx, int B, int T, hipStream_t s);
 void launch_zero32(void* p, size_t bytes, hipStream_t s);   // bytes: a multiple of 4
 template <typename S>

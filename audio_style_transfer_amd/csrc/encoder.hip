@@ -327,6 +327,49 @@ __global__ void __launch_bounds__(256) k_startconv_fwd(const float* __restrict__
     }
 }
 
+// Split mode's start conv (block 0 recomputes e_0 from x, FwdArgsS::xin): only the e_0 > 0 mask
+// words and the per-clip max |e_0|.  One row per lane, all 128 channels in a loop (W0 / b0 uniform:
+// scalar loads), the row's eight u16 words built in registers and stored as one 16-B piece
+// (64 lanes: 1 KiB contiguous) -- the same values as k_startconv_fwd's (e0_val, the same bit
+// layout), without its 16-lane-per-row shuffles (0.16 -> ~0.03 ms at 256 x 16384)
+__global__ void __launch_bounds__(256) k_startconv_masks(const float* __restrict__ x,
+                                                         const float* __restrict__ w0,
+                                                         const float* __restrict__ b0, int B, int T,
+                                                         uint16_t* __restrict__ me0,
+                                                         unsigned* __restrict__ gmax) {
+    // clip-interleaved block order (as k_startconv_fwd): concurrent workgroups, different clips
+    const int nper = T / SFR;
+    const size_t lb = (size_t)(blockIdx.x % B) * nper + blockIdx.x / B;
+    const size_t rowi = lb * SFR + threadIdx.x;
+    const int t = (int)(rowi % (size_t)T);
+    const float* xc = x + (rowi - t);
+    const float xm = t > 0 ? xc[t - 1] : 0.f, x0 = xc[t], xp = t + 1 < T ? xc[t + 1] : 0.f;
+    // word (h, Q) (u16 index 4 h + Q) holds channel 32 Q + 8 g + 4 h + j at bit mbit(4 g + j) =
+    // 4 j + g.  Chunks of 16 channels (a runtime loop: the whole W0 / b0 in scalar registers
+    // spilled): chunk k is Q = k / 2, g = 2 (k & 1) + i / 8 for its channel i
+    uint64_t P0 = 0, P1 = 0;   // words (0, Q) and (1, Q) at bits 16 Q
+    float amax = 0.f;
+#pragma unroll 1
+    for (int k = 0; k < C / 16; ++k) {
+        uint32_t wh0 = 0u, wh1 = 0u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int c = 16 * k + i;
+            const float o = e0_val(w0[c], w0[C + c], w0[2 * C + c], b0[c], xm, x0, xp);
+            amax = fmaxf(amax, fabsf(o));
+            const uint32_t bit = (o > 0.f ? 1u : 0u) << (4 * (i & 3) + (i >> 3));
+            if ((i >> 2) & 1) wh1 |= bit; else wh0 |= bit;
+        }
+        const int sh = 16 * (k >> 1) + 2 * (k & 1);
+        P0 |= (uint64_t)wh0 << sh;
+        P1 |= (uint64_t)wh1 << sh;
+    }
+    *reinterpret_cast<uint4*>(me0 + rowi * 8) =
+        make_uint4((uint32_t)P0, (uint32_t)(P0 >> 32), (uint32_t)P1, (uint32_t)(P1 >> 32));
+    amax = wave_max_f(amax);
+    if ((threadIdx.x & 63) == 0) atomicMax(gmax + blockIdx.x % B, __float_as_uint(amax));
+}
+
 // d loss / d x (startconv transposed, model.py:82-93, incl. the 1/128 of model.py:83):
 //   gx[t] = (1/128) sum_k a_k[t - k + 1],   a_k[t] = sum_c W0[k][c] g0[t][c].
 // One workgroup per SCB rows: the 16-B chunks of a row go to CPR consecutive lanes, which form
@@ -459,6 +502,11 @@ void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b
                           hipStream_t s, uint16_t* me0, unsigned* gmax) {
     hipLaunchKernelGGL(k_startconv_fwd<S>, dim3((unsigned)((size_t)B * T / SFR)), dim3(256), 0, s, x,
                        e0, w0, b0, B, T, me0, gmax);
+}
+void launch_startconv_masks(const float* x, const float* w0, const float* b0, int B, int T,
+                            hipStream_t s, uint16_t* me0, unsigned* gmax) {
+    hipLaunchKernelGGL(k_startconv_masks, dim3((unsigned)((size_t)B * T / SFR)), dim3(SFR), 0, s, x, w0,
+                       b0, B, T, me0, gmax);
 }
 void launch_startx_gx(const float* spart, float* gx, int B, int T, hipStream_t s) {
     const size_t n = (size_t)B * T;
