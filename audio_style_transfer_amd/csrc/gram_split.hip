@@ -430,6 +430,212 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
     }
 }
 
+// ---- backward over half rows (round 5): 64 channels per workgroup ----
+// The bare data movement of this backward runs ~5.6 % faster when a workgroup's row pieces are
+// 256 B (64 channels) instead of 128 B (tools/diag/gram_pattern.hip).  The S~
+// fragments of 64 channels double the registers of k_gram_bwd_s's waves, so the stages are 8
+// rows (half the staging registers; the 16x16x32 MFMA's columns 8..15 repeat rows 0..7 and are
+// dropped -- the Gram is HBM-bound) and the split goes straight into the image after the barrier.
+// 8 waves x 8 channels.  D is bit-identical to k_gram_bwd_s's (the same MFMAs per element, the
+// same K order); the fused content tap's squared errors go to 128-row slots, T / 128 x 2 =
+// ncpart partials per clip, each summed in a fixed order (thread over the slot's stages, wave
+// butterfly, waves 0..7), whatever the chunking.  Wave pair g = w >> 1 stages and stores the
+// tensors u = 8 g + k (k < 8): one set of 8 wave-uniform resources serves both.
+constexpr int HCH = 64;       // channels per workgroup
+constexpr int HSS = 8;        // rows per stage
+constexpr int HWT = 512;      // threads
+constexpr int HOR = 68;       // O row stride (floats; 16-B aligned)
+constexpr int HSLOT = 128;    // rows per content-error slot
+
+__device__ __forceinline__ void decode_h(const GramArgs& a, int& b, int& ch, int& c0) {
+    const int nwg = a.B * a.nchunk * 2;
+    int work = xcd_remap(blockIdx.x, nwg);   // the two channel halves of a chunk share one XCD
+    const int cgi = work & 1;
+    work >>= 1;
+    ch = work % a.nchunk;
+    b = work / a.nchunk;
+    c0 = cgi * HCH;
+}
+// raw buffer access: a tensor's clip base in a resource (scalar registers) + one 32-bit lane
+// offset shared by the 8 tensors of a thread (64-bit per-tensor lane addresses spilled); a
+// resource of 0 records (a padding tensor) reads zeros and drops its stores
+typedef unsigned int hu32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t h_rsrc(const void* p, bool real) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, real ? 0x7fffffff : 0, 0x00020000);
+}
+// image [c][t][u] (bf16): the 16-B block of K positions 8 g .. 8 g + 7 at block g ^ hswz(c, t),
+// so the staging writes (rows t & 3 x channel quads c >> 2 over 16 lanes) and the fragment
+// reads (rows 0..7 of one channel) are conflict-free
+__device__ __forceinline__ int hswz(int c, int t) { return ((c >> 2) ^ (t >> 2)) & 3; }
+
+template <bool CONT>
+__global__ void __launch_bounds__(HWT) k_gram_bwd_h(GramArgs a) {
+    __shared__ __attribute__((aligned(16))) u16 IH[HCH * HSS * 32];      // [c][t][u] hi
+    __shared__ __attribute__((aligned(16))) u16 IL[HCH * HSS * 32];      // [c][t][u] lo
+    __shared__ __attribute__((aligned(16))) float O[32 * HSS * HOR];     // [u][t][c]
+    __shared__ float cws[HWT / 64];
+    int b, ch, c0;
+    decode_h(a, b, ch, c0);
+    const int tlen = a.T / a.nchunk, tbeg = ch * tlen, tend = tbeg + tlen;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int i16 = lane & 15, kq = lane >> 4;
+    float omax = 0.f;   // max |D| of tensor top_u
+    float csd = 0.f;    // squared content error of tensor cont_u (this HSLOT-row slot)
+    // A fragments: S~_c[u = 16 m + i16][u' = 8 kq .. + 8] as bf16 hi / lo, c = c0 + 8 w + cc
+    uint4 sa[8][2][2];
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const float* sm = a.smat + ((size_t)b * C + c0 + 8 * w + cc) * 1024 + (16 * m + i16) * 32 + 8 * kq;
+            const float4 p = *reinterpret_cast<const float4*>(sm);
+            const float4 q = *reinterpret_cast<const float4*>(sm + 4);
+            uint32_t h[4], l[4];
+            split2(p.x, p.y, h[0], l[0]);
+            split2(p.z, p.w, h[1], l[1]);
+            split2(q.x, q.y, h[2], l[2]);
+            split2(q.z, q.w, h[3], l[3]);
+            sa[cc][m][0] = make_uint4(h[0], h[1], h[2], h[3]);
+            sa[cc][m][1] = make_uint4(l[0], l[1], l[2], l[3]);
+        }
+    // staging loads: tensors 8 g + k (k < 8, g = w >> 1: wave-uniform), channel quad sq, row st
+    // of the stage; a row piece of 64 channels = 16 lanes x 16 B
+    const int g = w >> 1, sq = lane >> 2, st = (lane & 3) + 4 * (w & 1);
+    __amdgpu_buffer_rsrc_t rs[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int u = 8 * g + k;
+        rs[k] = h_rsrc(u < a.nu ? (const float*)a.act + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C : (const float*)a.zero16, u < a.nu);
+    }
+    const uint32_t lofs = (uint32_t)(c0 + 4 * sq) * 4u;   // bytes
+    // fused content tap: the 128 threads whose output pieces (iteration cont_u & 7 of the store
+    // loop) are tensor cont_u's load its E and phi rows at the start of each stage
+    const int ctt = (tid >> 4) & 7, cq = tid & 15;
+    const bool cthr = CONT && g == (a.cont_u >> 3);
+    // iterations of the store loop (wave-uniform): tensors u = 8 g + it < nu; the content
+    // tensor's and the top tensor's (or -1)
+    const int nlive = min(max(a.nu - 8 * g, 0), 8);
+    const int cit = cthr ? a.cont_u & 7 : -1;
+    const int tit = a.top_u >= 0 && (a.top_u >> 3) == g ? a.top_u & 7 : -1;
+    __amdgpu_buffer_rsrc_t rce, rcp;   // the content tensor's clip and the clip's phi (+ cont_off)
+    if (CONT) {
+        rce = h_rsrc((const float*)a.act + (size_t)a.uid[a.cont_u & 31] * a.tstride + (size_t)b * a.T * C, true);
+        rcp = h_rsrc(a.cont_phi + (size_t)b * a.cont_phi_bstride + a.cont_off, true);
+    }
+    float4 vr[2][8];
+    // unconditional loads (past the chunk a stage re-reads the chunk's last stage, an L2 hit)
+    auto load = [&](float4 (&v)[8], int t0) {
+        const int tr = min(t0, tend - HSS);
+        const uint32_t vo = lofs + (uint32_t)(tr + st) * (C * 4);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs[k], vo, 0, 0));
+    };
+    auto stage = [&](float4 (&v)[8], int t0) {
+        float4 ce, cph = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (CONT && cthr) {
+            ce = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                rce, ((uint32_t)(t0 + ctt) * C + (uint32_t)(c0 + 4 * cq)) * 4u, 0, 0));
+            if (c0 + 4 * cq < a.cont_ncol)   // (phi rows hold only cont_ncol channels)
+                cph = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                    rcp, ((uint32_t)(t0 + ctt) * (uint32_t)a.cont_ncc + (uint32_t)(c0 + 4 * cq)) * 4u, 0, 0));
+        }
+        __syncthreads();   // the previous stage's image and O reads are done
+        // channel 4 sq + j: K positions 8 g .. 8 g + 7, split straight into the image
+#define HSPLIT(J) { uint4 fh, fl; const int c = 4 * sq + J; \
+        const int o = (c * HSS + st) * 32 + 8 * (g ^ hswz(c, st)); \
+        split8<J>(v, fh, fl); *reinterpret_cast<uint4*>(&IH[o]) = fh; *reinterpret_cast<uint4*>(&IL[o]) = fl; }
+        HSPLIT(0) HSPLIT(1) HSPLIT(2) HSPLIT(3)
+#undef HSPLIT
+        load(v, t0 + 2 * HSS);
+        __syncthreads();
+        // D_c = S~_c E_c for the wave's 8 channels; lane (i16, kq) holds D_c[16 m + 4 kq + i][i16 & 7]
+        const int tr8 = i16 & 7;
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) {
+            const int cl = 8 * w + cc;
+            const int o = (cl * HSS + tr8) * 32 + 8 * (kq ^ hswz(cl, tr8));
+            const uint4 bh = *reinterpret_cast<const uint4*>(&IH[o]);
+            const uint4 bl = *reinterpret_cast<const uint4*>(&IL[o]);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][0]),
+                                                             __builtin_bit_cast(bf16x8, bh), acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][1]),
+                                                             __builtin_bit_cast(bf16x8, bh), acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, sa[cc][m][0]),
+                                                             __builtin_bit_cast(bf16x8, bl), acc, 0, 0, 0);
+                // (lanes i16 >= 8 hold the same values as i16 - 8: they write them again, no branch)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) O[((16 * m + 4 * kq + i) * HSS + tr8) * HOR + cl] = acc[i];
+            }
+            __builtin_amdgcn_sched_barrier(0);   // one channel's fragments live at a time (registers)
+        }
+        float4 cadd = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (CONT && cthr) {
+            const int cc0 = c0 + 4 * cq;
+            const float ev[4] = {ce.x, ce.y, ce.z, ce.w}, pv[4] = {cph.x, cph.y, cph.z, cph.w};
+            float d[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                d[i] = cc0 + i < a.cont_ncol ? ev[i] - pv[i] : 0.f;
+                csd = fmaf(d[i], d[i], csd);
+            }
+            cadd = make_float4(a.cont_coef * d[0], a.cont_coef * d[1], a.cont_coef * d[2], a.cont_coef * d[3]);
+        }
+        __syncthreads();
+        // 32 tensors x 8 rows x 16 quads: tensor u = 8 g + it through its staging resource rs[it]
+        // (act and actw are the same buffer)
+        const uint32_t so = ((uint32_t)(t0 + ctt) * C + (uint32_t)(c0 + 4 * cq)) * 4u;
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int u = 8 * g + it;
+            if (it < nlive) {
+                float4 o = *reinterpret_cast<const float4*>(&O[(u * HSS + ctt) * HOR + 4 * cq]);
+                if (CONT && it == cit) { o.x += cadd.x; o.y += cadd.y; o.z += cadd.z; o.w += cadd.w; }
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hu32x4, o), rs[it], so, 0, 0);
+                if (it == tit)
+                    omax = fmaxf(omax, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+            }
+        }
+    };
+    load(vr[0], tbeg);
+    load(vr[1], tbeg + HSS);
+    auto flush_c = [&](int slot) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) csd += __shfl_xor(csd, off);
+        if (lane == 0) cws[w] = csd;
+        __syncthreads();
+        if (tid == 0) {
+            float v = 0.f;
+#pragma unroll
+            for (int k = 0; k < HWT / 64; ++k) v += cws[k];
+            a.cont_part[(size_t)b * a.cont_pstride + slot * (C / HCH) + c0 / HCH] = v;
+        }
+        csd = 0.f;
+    };
+    for (int t0 = tbeg; t0 < tend; t0 += 2 * HSS) {
+        stage(vr[0], t0);
+        if (CONT && (t0 + HSS) % HSLOT == 0) flush_c(t0 / HSLOT);
+        stage(vr[1], t0 + HSS);
+        if (CONT && (t0 + 2 * HSS) % HSLOT == 0) flush_c((t0 + HSS) / HSLOT);
+    }
+    if (a.top_u >= 0) {   // one atomic per workgroup
+        __shared__ float wm[HWT / 64];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) omax = fmaxf(omax, __shfl_xor(omax, off));
+        if (lane == 0) wm[w] = omax;
+        __syncthreads();
+        if (tid == 0) {
+            float m = wm[0];
+#pragma unroll
+            for (int k = 1; k < HWT / 64; ++k) m = fmaxf(m, wm[k]);
+            atomicMax(a.gmax_top + b, __float_as_uint(m));
+        }
+    }
+}
+
 // ---- fp32 mode (precision 0): the same staging and data movement on fp32 MFMA ----
 // forward: image [c][u][t] fp32 (row stride FRF floats: 80 B, conflict-free 16-B reads); the
 // symmetric Gram as three v_mfma_f32_16x16x4f32 tiles (U0 U0, U0 U1, U1 U1; U = 16 tensors) per
@@ -739,7 +945,38 @@ void launch_gram_bwd(const GramArgs& a, hipStream_t s) {
     if (has_cg) hipLaunchKernelGGL(k_gram_bwd_f<true>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
     else hipLaunchKernelGGL(k_gram_bwd_f<false>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
 }
-void launch_gram_bwd_s(const GramArgs& a, hipStream_t s) {
+// Chunks of the half-row backward: the fewest whole-slot chunks, at least 4, that give >= 4096
+// workgroups (depends on B and T only; the results do not depend on it)
+static int gram_bwd_h_chunks(int B, int T) {
+    const int slots = T / HSLOT;
+    int d = 1;
+    for (int k = 1; k <= slots; ++k) {
+        if (slots % k) continue;
+        d = k;
+        if (k >= 4 && (size_t)B * k * 2 >= 4096) break;
+    }
+    return d;
+}
+static bool gram_bwd_half() {   // ASTYLE_GRAM_BWD_H=0: the 32-channel kernel (A/B)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("ASTYLE_GRAM_BWD_H"); v = e ? (atoi(e) != 0) : 1; }
+    return v != 0;
+}
+bool gram_bwd_s_half(const GramArgs& a) {   // (a content-gradient buffer: the 32-channel kernel)
+    if (!gram_bwd_half() || a.T % HSLOT) return false;
+    for (int u = 0; u < a.nu; ++u) if (a.cg[u]) return false;
+    return true;
+}
+void launch_gram_bwd_s(const GramArgs& a0, hipStream_t s) {
+    if (gram_bwd_s_half(a0)) {
+        GramArgs a = a0;
+        a.nchunk = gram_bwd_h_chunks(a.B, a.T);
+        const dim3 grid(a.B * a.nchunk * 2);
+        if (a.cont_u >= 0) hipLaunchKernelGGL(k_gram_bwd_h<true>, grid, dim3(HWT), 0, s, a);
+        else hipLaunchKernelGGL(k_gram_bwd_h<false>, grid, dim3(HWT), 0, s, a);
+        return;
+    }
+    const GramArgs& a = a0;
     const dim3 grid(a.B * a.nchunk * (C / GCS));
     if (a.cont_u >= 0 && (a.T / a.nchunk) % GRAM_CSLOT) {
         fprintf(stderr, "gram_bwd_s: the fused content tap needs whole %d-row chunks\n", GRAM_CSLOT);

@@ -29,7 +29,8 @@ __device__ __forceinline__ float4 f(float4 v) {
 
 // MODE 0 quarter in place, 1 rows in place, 2 quarter out of place, 3 quarter read only,
 // 4 quarter over a channel-group-major layout [b][cg][t][32] in place, 5 the same read only,
-// 6 rows read only, 7 quarter in place with a barrier per stage
+// 6 rows read only, 7 quarter in place with a barrier per stage, 8 half rows (64 channels =
+// 256 B per row, two workgroups per chunk) read only, 9 half rows in place
 template <int MODE>
 __global__ void __launch_bounds__(512) kpat(float* act, float* out, float* sink) {
     extern __shared__ float dyn[];
@@ -43,11 +44,25 @@ __global__ void __launch_bounds__(512) kpat(float* act, float* out, float* sink)
     int tbeg, tlen;
     uint32_t lofs, rstep;   // lane offset, rows per stage
     int rowl;
+    const bool half = MODE == 8 || MODE == 9;
     const bool rows = MODE == 1 || MODE == 6;
     const bool cgm = MODE == 4 || MODE == 5;
-    const bool ro = MODE == 3 || MODE == 5 || MODE == 6;
+    const bool ro = MODE == 3 || MODE == 5 || MODE == 6 || MODE == 8;
     uint32_t rs = C;
-    if (rows) {
+    if (half) {
+        // workgroup (chunk, channel half, time half of the chunk): 16 tensors per thread-set
+        tlen = T / NCH / 2; tbeg = ch * (T / NCH) + (cg >> 1) * tlen;
+        const int uo = w & 1;
+        rowl = (lane >> 4) + 4 * (w >> 1);
+        lofs = 64 * (cg & 1) + 4 * (lane & 15);
+        rstep = GSS;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {   // (tensors 16 uo + 2 k .. : two per slot, see load)
+            const int u = 16 * uo + 2 * k;
+            ld[k] = u < NU ? act + (size_t)u * TSTRIDE + (size_t)b * T * C : act;
+            stp[k] = u < NU ? act + (size_t)u * TSTRIDE + (size_t)b * T * C : nullptr;
+        }
+    } else if (rows) {
         tlen = T / NCH / 4; tbeg = ch * (T / NCH) + cg * tlen;
         const int uo = w >> 1;
         rowl = (lane >> 5) + 2 * (w & 1);
@@ -75,7 +90,7 @@ __global__ void __launch_bounds__(512) kpat(float* act, float* out, float* sink)
             stp[k] = u < NU ? base + (size_t)u * TSTRIDE + (size_t)b * T * C + cb : nullptr;
         }
     }
-    float4 v[2][8];
+    float4 v[2][8], v2[2][8];
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     const int tend = tbeg + tlen;
     auto load = [&](float4 (&r)[8], int t0) {
@@ -83,11 +98,29 @@ __global__ void __launch_bounds__(512) kpat(float* act, float* out, float* sink)
 #pragma unroll
         for (int k = 0; k < 8; ++k) r[k] = *reinterpret_cast<const float4*>(ld[k] + lofs + (size_t)(tr + rowl) * rs);
     };
-    auto stage = [&](float4 (&r)[8], int t0) {
-        float4 o[8];
+    auto load2 = [&](float4 (&r)[8], int t0) {   // half mode: tensor u + 1 of each slot
+        const int tr = min(t0, tend - (int)rstep);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = f(r[k]);
+        for (int k = 0; k < 8; ++k)
+            r[k] = *reinterpret_cast<const float4*>(ld[k] + (16 * (w & 1) + 2 * k + 1 < NU ? TSTRIDE : 0) + lofs + (size_t)(tr + rowl) * rs);
+    };
+    auto stage = [&](float4 (&r)[8], float4 (&r2)[8], int t0) {
+        float4 o[8], o2[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { o[k] = f(r[k]); o2[k] = f(r2[k]); }
         load(r, t0 + 2 * rstep);
+        if (half) load2(r2, t0 + 2 * rstep);
+        if (half) {
+            if (ro) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) { acc.x += o2[k].x; acc.y += o2[k].y; acc.z += o2[k].z; acc.w += o2[k].w; }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (stp[k] && 16 * (w & 1) + 2 * k + 1 < NU)
+                        *reinterpret_cast<float4*>(stp[k] + TSTRIDE + lofs + (size_t)(t0 + rowl) * rs) = o2[k];
+            }
+        }
         if (MODE == 7) __syncthreads();
         if (ro) {
 #pragma unroll
@@ -100,11 +133,61 @@ __global__ void __launch_bounds__(512) kpat(float* act, float* out, float* sink)
     };
     load(v[0], tbeg);
     load(v[1], tbeg + rstep);
+    if (half) { load2(v2[0], tbeg); load2(v2[1], tbeg + rstep); }
     for (int t0 = tbeg; t0 < tend; t0 += 2 * rstep) {
-        stage(v[0], t0);
-        stage(v[1], t0 + rstep);
+        stage(v[0], v2[0], t0);
+        stage(v[1], v2[1], t0 + rstep);
     }
     if (ro && acc.x == 1234.5f) sink[tid] = acc.y + acc.z + acc.w + dyn[0];
+}
+
+// half rows with the register budget of a one-wave-per-SIMD kernel: 256 threads, 8-row stages,
+// thread (w, l): quad l & 15, row (l >> 4) + 4 (w & 1), tensors 16 (w >> 1) + k (k < 16)
+template <bool RO>
+__global__ void __launch_bounds__(256, 1) kpat_h256(float* act, float* sink) {
+    extern __shared__ float dyn[];
+    const int nwg = B * NCH * 4;
+    int work = xcd_remap(blockIdx.x, nwg);
+    const int cg = work % 4; work /= 4;
+    const int ch = work % NCH, b = work / NCH;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tlen = T / NCH / 2, tbeg = ch * (T / NCH) + (cg >> 1) * tlen, tend = tbeg + tlen;
+    const int rowl = (lane >> 4) + 4 * (w & 1);
+    const uint32_t lofs = 64 * (cg & 1) + 4 * (lane & 15);
+    float* base = act + (size_t)b * T * C;
+    const int u0 = 16 * (w >> 1);
+    float4 v[2][16];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto load = [&](float4 (&r)[16], int t0) {
+        const int tr = min(t0, tend - 8);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int u = u0 + k < NU ? u0 + k : 0;
+            r[k] = *reinterpret_cast<const float4*>(base + (size_t)u * TSTRIDE + lofs + (size_t)(tr + rowl) * C);
+        }
+    };
+    auto stage = [&](float4 (&r)[16], int t0) {
+        float4 o[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) o[k] = f(r[k]);
+        load(r, t0 + 16);
+        __syncthreads();
+        if (RO) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) { acc.x += o[k].x; acc.y += o[k].y; acc.z += o[k].z; acc.w += o[k].w; }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (u0 + k < NU) *reinterpret_cast<float4*>(base + (size_t)(u0 + k) * TSTRIDE + lofs + (size_t)(t0 + rowl) * C) = o[k];
+        }
+    };
+    load(v[0], tbeg);
+    load(v[1], tbeg + 8);
+    for (int t0 = tbeg; t0 < tend; t0 += 16) {
+        stage(v[0], t0);
+        stage(v[1], t0 + 8);
+    }
+    if (RO && acc.x == 1234.5f) sink[tid] = acc.y + acc.z + acc.w + dyn[0];
 }
 
 int main() {
@@ -137,16 +220,32 @@ int main() {
                err == hipSuccess ? "" : hipGetErrorString(err));
         fflush(stdout);
     };
-    const size_t ldss[2] = {118784, 80000};
+    auto run256 = [&](auto kern, const char* name, size_t lds, double rw) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(kern, dim3(B * NCH * 4), dim3(256), lds, 0, act, sink);
+        (void)hipDeviceSynchronize();
+        const int n = 6;
+        (void)hipEventRecord(e0, 0);
+        for (int i = 0; i < n; ++i) hipLaunchKernelGGL(kern, dim3(B * NCH * 4), dim3(256), lds, 0, act, sink);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        float ms;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        ms /= n;
+        printf("%-8s lds %6zu  %7.3f ms  %6.3f TB/s\n", name, lds, ms, rw * tb / (ms * 1e-3) / 1e12);
+        fflush(stdout);
+    };
+    const size_t ldss[1] = {118784};
     for (int rep = 0; rep < 2; ++rep)
         for (size_t lds : ldss) {
+            run256(kpat_h256<false>, "h256", 102400, 2.0);
+            run256(kpat_h256<true>, "h256_rd", 102400, 1.0);
             run(kpat<0>, "quarter", lds, 2.0);
-            run(kpat<7>, "q_sync", lds, 2.0);
+            run(kpat<9>, "half", lds, 2.0);
             run(kpat<1>, "rows", lds, 2.0);
-            run(kpat<4>, "cgmajor", lds, 2.0);
             run(kpat<3>, "read", lds, 1.0);
+            run(kpat<8>, "half_rd", lds, 1.0);
             run(kpat<6>, "rows_rd", lds, 1.0);
-            run(kpat<5>, "cgm_rd", lds, 1.0);
         }
     return 0;
 }
