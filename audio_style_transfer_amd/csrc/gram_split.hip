@@ -468,7 +468,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t h_rsrc(const void* p, bool rea
 // reads (rows 0..7 of one channel) are conflict-free
 __device__ __forceinline__ int hswz(int c, int t) { return ((c >> 2) ^ (t >> 2)) & 3; }
 
-template <bool CONT>
+// DOOP: D goes to a buffer of its own (actw != act, ASTYLE_DOOP=1): stores through resources of
+// their own (A/B only)
+template <bool CONT, bool DOOP>
 __global__ void __launch_bounds__(HWT) k_gram_bwd_h(GramArgs a) {
     __shared__ __attribute__((aligned(16))) u16 IH[HCH * HSS * 32];      // [c][t][u] hi
     __shared__ __attribute__((aligned(16))) u16 IL[HCH * HSS * 32];      // [c][t][u] lo
@@ -507,6 +509,14 @@ __global__ void __launch_bounds__(HWT) k_gram_bwd_h(GramArgs a) {
     for (int k = 0; k < 8; ++k) {
         const int u = 8 * g + k;
         rs[k] = h_rsrc(u < a.nu ? (const float*)a.act + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C : (const float*)a.zero16, u < a.nu);
+    }
+    __amdgpu_buffer_rsrc_t rsw[DOOP ? 8 : 1];
+    if (DOOP) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int u = 8 * g + k;
+            rsw[k] = h_rsrc(u < a.nu ? (const float*)a.actw + (size_t)a.uid[u] * a.tstride + (size_t)b * a.T * C : (const float*)a.zero16, u < a.nu);
+        }
     }
     const uint32_t lofs = (uint32_t)(c0 + 4 * sq) * 4u;   // bytes
     // fused content tap: the 128 threads whose output pieces (iteration cont_u & 7 of the store
@@ -586,7 +596,7 @@ __global__ void __launch_bounds__(HWT) k_gram_bwd_h(GramArgs a) {
         }
         __syncthreads();
         // 32 tensors x 8 rows x 16 quads: tensor u = 8 g + it through its staging resource rs[it]
-        // (act and actw are the same buffer)
+        // (in place: act and actw are the same buffer)
         const uint32_t so = ((uint32_t)(t0 + ctt) * C + (uint32_t)(c0 + 4 * cq)) * 4u;
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
@@ -594,7 +604,7 @@ __global__ void __launch_bounds__(HWT) k_gram_bwd_h(GramArgs a) {
             if (it < nlive) {
                 float4 o = *reinterpret_cast<const float4*>(&O[(u * HSS + ctt) * HOR + 4 * cq]);
                 if (CONT && it == cit) { o.x += cadd.x; o.y += cadd.y; o.z += cadd.z; o.w += cadd.w; }
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hu32x4, o), rs[it], so, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hu32x4, o), DOOP ? rsw[DOOP ? it : 0] : rs[it], so, 0, 0);
                 if (it == tit)
                     omax = fmaxf(omax, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
             }
@@ -972,8 +982,14 @@ void launch_gram_bwd_s(const GramArgs& a0, hipStream_t s) {
         GramArgs a = a0;
         a.nchunk = gram_bwd_h_chunks(a.B, a.T);
         const dim3 grid(a.B * a.nchunk * 2);
-        if (a.cont_u >= 0) hipLaunchKernelGGL(k_gram_bwd_h<true>, grid, dim3(HWT), 0, s, a);
-        else hipLaunchKernelGGL(k_gram_bwd_h<false>, grid, dim3(HWT), 0, s, a);
+        const bool doop = a.actw != a.act;
+        if (a.cont_u >= 0) {
+            if (doop) hipLaunchKernelGGL((k_gram_bwd_h<true, true>), grid, dim3(HWT), 0, s, a);
+            else hipLaunchKernelGGL((k_gram_bwd_h<true, false>), grid, dim3(HWT), 0, s, a);
+        } else {
+            if (doop) hipLaunchKernelGGL((k_gram_bwd_h<false, true>), grid, dim3(HWT), 0, s, a);
+            else hipLaunchKernelGGL((k_gram_bwd_h<false, false>), grid, dim3(HWT), 0, s, a);
+        }
         return;
     }
     const GramArgs& a = a0;
