@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-5 A/B on the GPU box: quick benches of the round-4 build (tools/_r4, its own bench.py)
-# and of this tree.  usage: tools/r5ab.sh "tag|ENV=v ENV2=w|bench args" ...  (a tag starting
-# with r4 runs the round-4 tree)
+# Round-5 A/B on the GPU box: quick benches of this tree under different settings / libraries
+# (ASTYLE_LIB=...), and of a round-4 build checked out at tools/_r4 (git worktree of round 4's
+# last commit; not kept in the tree).  usage: tools/r5ab.sh "tag|ENV=v ENV2=w|bench args" ...
+# (a tag starting with r4 runs the round-4 tree)
 set -o pipefail
 mkdir -p gpurun_out
 for v in "$@"; do
