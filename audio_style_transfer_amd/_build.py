@@ -54,15 +54,19 @@ def build_variant(name: str = 'fwdvariants', force: bool = False) -> str:
     extra = [os.path.join(VARIANTS, f) for f in VARIANT_SOURCES.get(name, ([], []))[0]]
     if not force and not _stale(lib, extra):
         return lib
-    old = os.environ.get('ASTYLE_VARIANT')
+    # built from VARIANT_SOURCES' own defines only: an ASTYLE_DEFS of the caller's environment
+    # (e.g. a diagnostic define) must not leak into it
+    old = {k: os.environ.get(k) for k in ('ASTYLE_VARIANT', 'ASTYLE_DEFS')}
     os.environ['ASTYLE_VARIANT'] = name
+    os.environ.pop('ASTYLE_DEFS', None)
     try:
         return build(force=True)
     finally:
-        if old is None:
-            del os.environ['ASTYLE_VARIANT']
-        else:
-            os.environ['ASTYLE_VARIANT'] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = False) -> str:

@@ -173,7 +173,7 @@ def run_rank(args, pairs, ws, rank, dev, log=print):
         if not run.any():
             break
         x0 = x.astype(np.float32).astype(np.float64)                # each epoch from fp32(x)
-        xe, hist = np.empty_like(x), [None] * B
+        xe, hist, nev = np.empty_like(x), [None] * B, np.zeros(B, np.int64)
         # one minimize call per precision; the split clips first, so the clips its range guard
         # flags join this epoch's single fp32 call (from the same x0) beside the clips already
         # on fp32, and every clip's result is taken from the one call that ran it
@@ -194,11 +194,11 @@ def run_rank(args, pairs, ws, rank, dev, log=print):
                     pending['fp32'] = pending['fp32'] | bad
                     sel = sel & ~bad
             for b in np.flatnonzero(sel):
-                xe[b], hist[b] = xs[b], hs[b]
+                xe[b], hist[b], nev[b] = xs[b], hs[b], info[b, 2]
         tl = time.time() - since     # the epoch's end: the device evaluations are not host-timed
         for b in np.flatnonzero(run):
             h = hist[b]
-            n = len(h)
+            n = int(nev[b])          # the clip's evaluation count (ast_lbfgs_state), = len(h)
             x[b] = xe[b]
             for k, pv in enumerate(h):                               # methods.py:147-157
                 writers[b].add_scalars({'loss/content_loss': pv[1], 'loss/style_loss': pv[2],

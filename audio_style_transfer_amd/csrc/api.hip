@@ -1203,6 +1203,10 @@ int ast_lbfgs_begin(ast_ctx* x, void* ws, float* xd, const double* x0, const int
     if (!x || !ws || !xd) return fail(AST_E_ARG, "null argument");
     if (m < 1 || m > 32) return fail(AST_E_ARG, "L-BFGS-B history m must be in 1..32");
     if (maxiter < 1 || maxls < 1) return fail(AST_E_ARG, "maxiter and maxls must be >= 1");
+    // every evaluation of the call must fit the per-call loss history (ast_lbfgs_history): at
+    // most 1 + maxiter (maxls + 1) of them
+    if ((long long)maxiter * (maxls + 1) + 1 > lbfgs_history_cap())
+        return fail(AST_E_ARG, "maxiter * (maxls + 1) + 1 exceeds AST_LBFGS_HISTORY evaluations");
     const bool known = std::find(x->lb_ws.begin(), x->lb_ws.end(), ws) != x->lb_ws.end();
     if (!x0 && !known)
         return fail(AST_E_STATE, "continuing (x0 NULL) needs a workspace started with x0");

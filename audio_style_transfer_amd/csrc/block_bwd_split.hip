@@ -71,6 +71,14 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
 
     auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, a.ft, a.fn, a.d, ly); };
     auto clampt = [&](int tl) { return tl < ntiles ? tl : ntiles - 1; };
+#ifdef ASTYLE_DIAG_BWD_L2ROWS
+    // diagnostic build only (tools): every row load and store addresses the workgroup's first
+    // tile, so the same instruction stream runs from L2 instead of HBM (results wrong)
+    const Tile t0f = tile_of(blockIdx.x);
+    auto memt = [&](const Tile& t) { (void)t; return t0f; };
+#else
+    auto memt = [&](const Tile& t) { return t; };
+#endif
 
     // this wave's split weight halves (A: rows = channels 32 w.., K = the other side's channels)
     uint4 wr[8][2], wd[3][8][2];
@@ -125,13 +133,15 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     float4 lt[NU], lg[NU];
     // unmasked layouts load through buffer resources of the tile (rs_t / rs_d, set with the tile)
     rsrc_t rs_t, rs_d;
-    auto set_rs = [&](const Tile& t) {
+    auto set_rs = [&](const Tile& t_) {
+        const Tile t = memt(t_);
         if (!MASKED) {
             rs_t = ru.rsrc_of(a.tin, t, a.T, a.d);
             if (HAS_D) rs_d = ru.rsrc_of(a.dadd, t, a.T, a.d);
         }
     };
-    auto load_unit = [&](const Tile& t, int k) {
+    auto load_unit = [&](const Tile& t_, int k) {
+        const Tile t = memt(t_);
         if (MASKED) {
             lt[k] = ru.load(a.tin, t, k, a.T, a.fn, a.d);
             if (HAS_D) lg[k] = ru.load(a.dadd, t, k, a.T, a.fn, a.d);
@@ -284,7 +294,8 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
     float4 oe, oo;
     float sk0 = 0.f, sk1 = 0.f, sk2 = 0.f;   // SX: the lane's dot products over its 16 channels
     size_t sxo = 0;                          // SX: spart float index of (column, wave)
-    auto epi_begin = [&](const Tile& et, int J) {
+    auto epi_begin = [&](const Tile& et_, int J) {
+        const Tile et = memt(et_);
         if (SX) sxo = (((size_t)et.b * a.T + ctime(et, 32 * J + r, toff[J])) * 4 + w) * 4;
         else if (MASKED) dst = a.gout + ((size_t)et.b * a.T + ctime(et, 32 * J + r, toff[J])) * C + chb;
         else { rs_o = mk_rsrc(a.gout + ((size_t)et.b * a.T + et.tb) * C); ocol = colo[J]; }

@@ -373,7 +373,13 @@ __global__ void __launch_bounds__(256) k_gatys_fwd_s(GatysArgs a) {
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
     };
     // the diagonal / off-diagonal waves run separate copies of the loop (DIAG a constant in
-    // each), so the accumulators keep their registers across iterations
+    // each), so the accumulators keep their registers across iterations.
+    // Barrier invariant: waves 0-1 and 2-3 reach different s_barrier instructions,
+    // which is sound because s_barrier counts waves, not instruction addresses, and both copies
+    // execute the same number of barriers: `diag` is wave-uniform (w is readfirstlane'd), every
+    // wave runs exactly one copy, and in both copies the trip counts (nring, the NST - 1
+    // remainder stages) depend on nt and NST only, with exactly two __syncthreads per stage
+    // and none elsewhere.  Any change that gives DIAG its own barrier or trip count breaks this.
     auto run = [&](auto diag_tag) {
         constexpr bool DIAG = decltype(diag_tag)::value;
         auto stage = [&](float4 (&v)[8], int k) {

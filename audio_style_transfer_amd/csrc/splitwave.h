@@ -116,11 +116,19 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 __device__ __forceinline__ rsrc_t mk_rsrc(const void* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
 }
+// cache-policy bits of the block kernels' row loads / stores (gfx950 CPol: 2 = nt); A/B builds
+// only (ASTYLE_DEFS=-DSW_LD_AUX=2 ...), the shipped kernels use the default policy
+#ifndef SW_LD_AUX
+#define SW_LD_AUX 0
+#endif
+#ifndef SW_ST_AUX
+#define SW_ST_AUX 0
+#endif
 __device__ __forceinline__ float4 bld4(rsrc_t r, uint32_t voff, uint32_t soff) {
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, SW_LD_AUX));
 }
 __device__ __forceinline__ void bst4(rsrc_t r, uint32_t voff, uint32_t soff, float4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, SW_ST_AUX);
 }
 
 __device__ __forceinline__ uint4 lds16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }

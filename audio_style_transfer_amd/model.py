@@ -38,6 +38,10 @@ class cfg(object):
         x = x.to(dev).contiguous()
         B, T = x.shape
         if self._engine is None or (self._engine.batch, self._engine.T) != (B, T):
+            # a new (B, T) needs a context of its own: the old one's device workspace (76 GB at
+            # B = 256) is released now, not whenever the garbage collector gets to it (extracts
+            # are copies, so nothing the caller holds points into it)
+            self.close()
             # taps 29 (content) + 31 (bottleneck) and style 0 + 30 make every block run
             self._engine = StyleEngine(B, T, [29, 31], [0, 30], cnt_channels=16,
                                        precision=self.precision, device=dev, weights=self.weights)
@@ -47,3 +51,9 @@ class cfg(object):
         enc = torch.nn.functional.avg_pool1d(bott.transpose(1, 2), self.ae_hop_length,
                                              self.ae_hop_length).transpose(1, 2)
         return {'quantized_input': x, 'encoding': enc, 'before_enc': self.extracts[30]}
+
+    def close(self):
+        """Destroy the library context (its device workspace); build() makes a new one."""
+        if self._engine is not None:
+            self._engine.close()
+            self._engine = None

@@ -373,6 +373,65 @@ def block_roofline(precision, B, T, fwd_ms, bwd_ms, traffic, ms_per_step, gram_m
     return roof
 
 
+def gram_roofline(precision, gatys, B, T, L, fwd_ms, bwd_ms, traffic):
+    """The Gram kernels against both roofs (the north_star asks for their MFMA
+    utilisation against the gfx950 peak).  Bytes per launch: the forward reads the L tapped
+    tensors, the backward reads and writes them (D in place).  FLOP per time row:
+    algorithmic = the reference's matmuls (methods.py:68-76): ours G_c = E_c E_c^T per channel,
+    2 L^2 128; Gatys G_l = F_l^T F_l per layer, 2 128^2 L (forward and backward alike).
+    executed = what the MFMA pipe issues in the split kernels (gram_split.hip, gram_gatys.hip):
+    three bf16 products per product; ours pads L to 32 tensors, and its half-row backward
+    (k_gram_bwd_h) computes every 16x16x32 tile on 8 real rows (columns 8..15 repeat rows
+    0..7); the Gatys forward computes the 10 upper 32x32 tiles of the symmetric 128 x 128 (10/16).
+    mfma_frac_at_hbm_roof = executed FLOP per HBM byte x 8 TB/s / the bf16 peak: the MFMA
+    utilisation these kernels would reach at the HBM roofline, the ceiling of mfma_frac."""
+    esz = 2.0 if precision == 'bf16' else 4.0
+    rows = float(B) * T
+    A = rows * 128 * esz
+    tf = traffic or {}
+    split = precision == 'split'
+    peak = FP32_MFMA_PEAK_TFLOPS if precision == 'fp32' else F16_MFMA_PEAK_TFLOPS
+    if gatys:
+        alg = 2.0 * 128 * 128 * L
+        ex_f = 3 * alg * 10 / 16 if split else None
+        ex_b = 3 * alg if split else None
+        names = ('k_gatys_fwd_s', 'k_gatys_bwd_s2') if split else ('gatys fwd', 'gatys bwd')
+    else:
+        alg = 2.0 * L * L * 128
+        ex_f = 3 * 2.0 * 32 * 32 * 128 if split else None
+        half = os.environ.get('ASTYLE_GRAM_BWD_H', '1') != '0'
+        ex_b = 3 * 2.0 * 32 * 32 * 128 * (2 if half else 1) if split else None
+        names = ('k_gram_fwd_s', 'k_gram_bwd_h' if half else 'k_gram_bwd_s') if split else \
+            ('gram fwd', 'gram bwd')
+
+    def one(name, ms, nbytes, ex, tb):
+        sec = ms * 1e-3
+        d = {'kernel': name, 'launch_ms': ms, 'algorithmic_bytes': nbytes,
+             'achieved_GBs': nbytes / sec / 1e9, 'hbm_frac': nbytes / sec / 1e9 / HBM_PEAK_GBS,
+             'traffic': tb, 'algorithmic_flops': alg * rows,
+             'algorithmic_TFLOPs': alg * rows / sec / 1e12}
+        if ex is not None:
+            d.update(executed_mfma_flops=ex * rows, mfma_TFLOPs=ex * rows / sec / 1e12,
+                     mfma_frac=ex * rows / sec / 1e12 / peak,
+                     mfma_frac_at_hbm_roof=ex * rows / nbytes * HBM_PEAK_GBS / 1e3 / peak)
+        return d
+    f = one(names[0], fwd_ms, L * A, ex_f, tf.get('gram_fwd'))
+    b = one(names[1], bwd_ms, 2 * L * A, ex_b, tf.get('gram_bwd'))
+    return {'bound': 'hbm', 'peak': HBM_PEAK_GBS, 'mfma_peak_TFLOPs': peak,
+            'fwd_achieved_GBs': f['achieved_GBs'], 'bwd_achieved_GBs': b['achieved_GBs'],
+            'fwd_frac': f['hbm_frac'], 'bwd_frac': b['hbm_frac'],
+            'fwd_traffic': f['traffic'], 'bwd_traffic': b['traffic'],
+            'fwd_mfma_frac': f.get('mfma_frac'), 'bwd_mfma_frac': b.get('mfma_frac'),
+            'fwd': f, 'bwd': b,
+            'note': ('HBM-bound: %.0f / %.0f algorithmic flop per HBM byte (fwd / bwd; SURVEY F9), '
+                     'so even at 8 TB/s the MFMA utilisation stays at mfma_frac_at_hbm_roof '
+                     '(executed, %s) -- the north_star\'s >= 50 %% MFMA is out of reach for this '
+                     'Gram; the HBM fractions are its roofline'
+                     % (alg / (128 * esz * L), alg / (2 * 128 * esz * L),
+                        'fwd %.2f / bwd %.2f' % (f['mfma_frac_at_hbm_roof'], b['mfma_frac_at_hbm_roof'])
+                        if split else 'n/a'))}
+
+
 def rank_main(args):
     import torch
     ws, rank, dev = dist_setup(args)
@@ -400,6 +459,8 @@ def rank_main(args):
                                       'note': 'configs[1]: 1 clip x %d, channel-wise Gram, 30 '
                                               'blocks, %s' % (T, PREC_NOTE[p])}
         side['lbfgs_mode'] = run_lbfgs(args, Eng, 2 * args.side_steps, dev)
+        if not args.gatys and args.engine == ap_default_engine():
+            side['reference_protocol'] = reference_protocol(T, dev)
     if rank != 0:
         barrier(ws)
         return None
@@ -449,13 +510,8 @@ def rank_main(args):
                                 'block_bwd': tm['block_bwd_ms'] / calls,
                                 'gram_fwd': gram_fwd_ms, 'gram_bwd': gram_bwd_ms,
                                 'other': tm['other_ms'] / calls},
-        'gram_roofline': {'bound': 'hbm', 'fwd_achieved_GBs': gbytes / (gram_fwd_ms * 1e-3) / 1e9,
-                          'bwd_achieved_GBs': 2 * gbytes / (gram_bwd_ms * 1e-3) / 1e9,
-                          'fwd_frac': gbytes / (gram_fwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                          'bwd_frac': 2 * gbytes / (gram_bwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                          'peak': HBM_PEAK_GBS,
-                          'fwd_traffic': (traffic or {}).get('gram_fwd'),
-                          'bwd_traffic': (traffic or {}).get('gram_bwd')},
+        'gram_roofline': gram_roofline(args.precision, args.gatys, Bt, T, L, gram_fwd_ms,
+                                       gram_bwd_ms, traffic),
         'loss_first_last': [first_loss, last_loss],
         'nonfinite_clips': bad[0],
         'range_flagged_clips': bad[1],
@@ -465,9 +521,78 @@ def rank_main(args):
     out.update(side)
     if ws == 1 and args.cpu_baseline_seconds > 0:
         out['cpu_baseline'] = cpu_baseline(T, args.cpu_baseline_seconds, args.gatys)
+        rp = out.get('reference_protocol')
+        if rp:   # the drop-in's one-clip rate beside the CPU path's, same protocol
+            cpu = out['cpu_baseline']['config1_iters_per_s']
+            rp['cpu_baseline_config1_evals_per_s'] = cpu
+            rp['config1_scipy_vs_cpu_baseline'] = rp['config1']['scipy']['evals_per_s'] / cpu
     print(json.dumps(out), flush=True)
     barrier(ws)
     return out
+
+
+def ap_default_engine():
+    return parse([]).engine
+
+
+def reference_protocol(T, dev, maxiter=100):
+    """The drop-in on the reference's own protocol: GatysNet.l_bfgs for one
+    epoch (one minimize call, maxiter 100) of ONE clip of T samples from x = 1e-6
+    (methods.py:49-54,132-137,164-181), as a user of methods.py runs it: 'scipy' = host scipy
+    L-BFGS-B with one H2D copy of x and one D2H copy of the gradient and loss parts per
+    evaluation (the reference's ScipyOptimizerInterface round trip); 'device' = the same L-BFGS-B
+    in device memory (ast_lbfgs_*).  configs[0]'s taps (stack 0 = style layers 0..9, content
+    layer 25) and configs[1]'s (the CLI defaults: style layers 0..29, content layer 29), lambd
+    100, gamma 0, split precision, synthetic clips (content seed 1000, style 5000).  host_share
+    = 1 - evaluations x device time of one resident ast_loss_grad / epoch wall time: the part
+    of the epoch spent in scipy, the copies and Python."""
+    import tempfile
+    import torch
+    from audio_style_transfer_amd.methods import GatysNet
+    from audio_style_transfer_amd.weights import synthetic_weights, synthetic_clips
+    W = synthetic_weights(0)
+    cont, sty = synthetic_clips(1, T, 1000)[0], synthetic_clips(1, T, 5000)[0]
+    res = {}
+    for tag, stack, cids in (('config0', 0, [25]), ('config1', None, [29])):
+        with tempfile.TemporaryDirectory() as d:
+            net = GatysNet(d, None, os.path.join(d, 'log'), os.path.join(d, 'fig'), stack=stack,
+                           batch_size=T, cont_lyr_ids=cids, weights=W, plots=False)
+            phi_c = net.get_embeds(cont)
+            phi_s = net.get_embeds(sty, is_content=False)   # one-clip analogy: l2norm(G_s)
+            eng = net.engine
+            eng.set_targets(torch.as_tensor(phi_c), torch.as_tensor(phi_s))
+            xd = torch.full((1, T), 1e-6, device=dev)
+            for _ in range(3):
+                eng.loss_grad(xd)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(20):
+                eng.loss_grad(xd)
+            torch.cuda.synchronize()
+            dev_ms = (time.perf_counter() - t0) / 20 * 1e3
+            r = {'style_layers': net.style_lyr_ids[0:1] + ['..'] + net.style_lyr_ids[-1:],
+                 'cont_layers': cids, 'device_ms_per_eval': dev_ms}
+            for opt in ('scipy', 'device'):
+                # an untimed 2-iteration call first: one-time costs (event writer, the device
+                # loop's workspace and code objects, scipy's first call) stay out of the epoch
+                net.l_bfgs(phi_c, phi_s, 1, 100.0, 0.0, optimizer=opt, maxiter=2,
+                           log=lambda *a: None)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                net.l_bfgs(phi_c, phi_s, 1, 100.0, 0.0, optimizer=opt, maxiter=maxiter,
+                           log=lambda *a: None)
+                torch.cuda.synchronize()
+                el = time.perf_counter() - t0
+                n = len(net.history)
+                r[opt] = {'evals': n, 'seconds_per_epoch': el, 'evals_per_s': n / el,
+                          'host_share': max(0.0, 1.0 - n * dev_ms * 1e-3 / el),
+                          'final_loss': float(net.history[-1][0])}
+            net.engine.close()
+        res[tag] = r
+    res['note'] = ('GatysNet.l_bfgs, one epoch (maxiter %d) of one %d-sample clip from x = 1e-6, '
+                   'wall time incl. per-epoch outputs (ep-0.wav, event file, state.npz); evals = '
+                   'loss+grad evaluations of the epoch' % (maxiter, T))
+    return res
 
 
 def run_lbfgs(args, Eng, steps, dev):

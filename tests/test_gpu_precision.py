@@ -13,8 +13,10 @@ relu pattern (oracle/masked_oracle.py; the pattern is rebuilt from the run's ext
   * arithmetic: |g_run - g_fp64[run masks]| <= 2x its measured value (the precision claim);
   * lottery: every decision the run takes differently from fp64 is a near-tie,
     |fp64 value| <= 1e-6 x max |layer|;
-and the total error <= 2x the value measured on HEAD (round 5), so a new flip or lost bits
-show up.  Measured (round 5, split / fp32): smoke arithmetic 4.21e-5 / 4.94e-6, total 3.14e-4 /
+and the total error <= the arithmetic bar + 1e-3 per flip (a flip moves the gradient by at most
+7e-4 on these problems), so a harmless reordering that flips other near-ties passes while lost
+bits or a flip that is no near-tie fail (round 5 held the total to 2x one lottery
+draw).  Measured (round 5, split / fp32): smoke arithmetic 4.21e-5 / 4.94e-6, total 3.14e-4 /
 3.37e-4 (one flip: u_22 / e_25); golden arithmetic 7.55e-6 / 9.96e-7, total 2.63e-5 / 2.28e-4.
 Round 3's build measured the same arithmetic (4.20e-5, 7.53e-6) with other flips.
 """
@@ -31,13 +33,14 @@ from audio_style_transfer_amd.weights import synthetic_clips
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-# (case, mode): (arithmetic bar, total bar) = 2x the round-5 measurement
+# (case, mode): arithmetic bar = 2x the round-5 measurement
 BARS = {
-    ('smoke', 'split'): (8.5e-5, 6.3e-4),
-    ('smoke', 'fp32'): (1.0e-5, 6.8e-4),
-    ('golden', 'split'): (1.5e-5, 5.3e-5),
-    ('golden', 'fp32'): (2.0e-6, 4.6e-4),
+    ('smoke', 'split'): 8.5e-5,
+    ('smoke', 'fp32'): 1.0e-5,
+    ('golden', 'split'): 1.5e-5,
+    ('golden', 'fp32'): 2.0e-6,
 }
+FLIP_ALLOWANCE = 1e-3   # per near-tie relu flip (measured 1e-4 .. 7e-4 each)
 
 
 def _case(name, W):
@@ -85,7 +88,7 @@ def test_gradient_error_is_arithmetic_plus_near_tie_flips(case, mode, weights):
             for t, c in np.argwhere(mh[k][l] != m64[k][l]):
                 ties.append((kind, l, int(t), int(c), abs(ref[t, c]) / np.abs(ref).max()))
     print('%s %s: total %.3e arithmetic %.3e flips %s' % (case, mode, total, arith, ties))
-    a_bar, t_bar = BARS[(case, mode)]
+    a_bar = BARS[(case, mode)]
     assert arith <= a_bar, (arith, a_bar)
     assert all(r <= 1e-6 for *_, r in ties), ties
-    assert total <= t_bar, (total, t_bar, ties)
+    assert total <= a_bar + FLIP_ALLOWANCE * len(ties), (total, a_bar, ties)

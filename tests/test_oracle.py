@@ -151,9 +151,12 @@ def test_masked_oracle_on_its_own_masks_is_the_oracle(weights, golden):
 
 def test_relu_lottery_explains_the_fp32_gradient_error(weights, golden):
     """The mechanism behind the gradient errors the GPU tests bound: an
-    fp32 restatement of the golden 'ours' case lands on the other side of 2 relu decisions whose
-    fp64 values are ~1e-7 of their layer's max (e_19, e_24); those 2 flips alone move the
-    gradient 6.3e-4, while the fp32 arithmetic on the same linear piece is 7.4e-7 from fp64."""
+    fp32 restatement of the golden 'ours' case lands on the other side of a few relu decisions
+    whose fp64 values are ~1e-7 of their layer's max (on the build that measured it: 2 flips,
+    e_19 and e_24, moving the gradient 6.3e-4, with the fp32 arithmetic on the same linear piece
+    7.4e-7 from fp64).  Which near-ties flip depends on the BLAS backend's rounding, so only the
+    mechanism is asserted: every flip is a near-tie, the arithmetic is fp32-class, and the total
+    is the arithmetic plus at most 1e-3 per flip."""
     from oracle import masked_oracle as M
     tg = np.load(os.path.join(GOLD, 'oracle_T2048_targets.npz'))
     kw = dict(cont_ids=[25], style_ids=list(range(30)))
@@ -163,10 +166,14 @@ def test_relu_lottery_explains_the_fp32_gradient_error(weights, golden):
     _, g32, _, m32 = M.loss_and_grad(x, weights, phi_c=pc, phi_s=ps, dtype=np.float32, **kw)
     _, gm, _, _ = M.loss_and_grad(x, weights, phi_c=pc, phi_s=ps, me=m32[0], mu=m32[1], **kw)
     fe, fu = M.flips(m32, m64)
-    assert sum(fe) + sum(fu) == 2
+    nflip = sum(fe) + sum(fu)
+    assert nflip <= 20
     cache = M.forward(x, weights)[1]
     for l in range(30):
-        for t, c in np.argwhere(m32[0][l] != m64[0][l]):
+        for t, c in np.argwhere(m32[0][l] != m64[0][l]):      # e_l > 0 decisions
             assert abs(cache['es'][l][t, c]) < 1e-6 * np.abs(cache['es'][l]).max()
-    assert 4e-4 < M.rel(gm, g64) < 9e-4          # the lottery
-    assert M.rel(g32, gm) < 2e-6                  # the arithmetic
+        for t, c in np.argwhere(m32[1][l] != m64[1][l]):      # u_l > 0 decisions
+            assert abs(cache['us'][l][t, c]) < 1e-6 * np.abs(cache['us'][l]).max()
+    arith = M.rel(g32, gm)
+    assert arith < 2e-6                                        # the arithmetic
+    assert M.rel(g32, g64) <= arith + 1e-3 * nflip + 1e-6      # + the lottery
