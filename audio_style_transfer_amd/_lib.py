@@ -17,7 +17,7 @@ RANGE_NONFINITE, RANGE_ACT, RANGE_GRAD, RANGE_TINY = 1, 2, 4, 8
 LBFGS_HISTORY = 4096    # AST_LBFGS_HISTORY: evaluations per minimize call kept for ast_lbfgs_history
 
 # Every symbol include/astyle.h declares (checked by tests/test_abi.py).
-EXPORTS = ('ast_create', 'ast_destroy', 'ast_workspace_bytes', 'ast_set_weight', 'ast_forward',
+EXPORTS = ('ast_create', 'ast_destroy', 'ast_workspace_bytes', 'ast_d_out_of_place', 'ast_set_weight', 'ast_forward',
            'ast_get_extract', 'ast_embeds', 'ast_content_cols', 'ast_set_targets',
            'ast_set_gamma', 'ast_loss_grad', 'ast_loss_grad_phase', 'ast_range_flags', 'ast_range_flags_last', 'ast_range_flags_reset', 'ast_set_cu_limit', 'ast_adam_step', 'ast_adam_step_dev',
            'ast_lbfgs_workspace_bytes', 'ast_lbfgs_begin', 'ast_lbfgs_step', 'ast_lbfgs_state',
@@ -59,6 +59,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         'ast_create': (i, [ctypes.POINTER(AstCfg), i, ctypes.POINTER(vp)]),
         'ast_destroy': (None, [vp]),
         'ast_workspace_bytes': (i, [ctypes.POINTER(AstCfg), ctypes.POINTER(sz)]),
+        'ast_d_out_of_place': (i, [vp, ctypes.POINTER(i), vp]),
         'ast_set_weight': (i, [vp, ctypes.c_char_p, fp, sz]),
         'ast_forward': (i, [vp, vp, vp]),
         'ast_get_extract': (i, [vp, i, vp, vp]),

@@ -121,7 +121,9 @@ struct ast_ctx {
     unsigned* gmax_g = nullptr;             // [nblk + 1][B] max |d loss / d e_l| per clip
     size_t esz = 4;                         // bytes per stored element
     void* act = nullptr; size_t tstride = 0;
-    void* dgrad = nullptr;   // style-tapped tensors' D out of place (ASTYLE_DOOP=1; default: in place over act)
+    void* dgrad = nullptr;   // style-tapped tensors' D out of place (doop; else in place over act)
+    bool doop = false;       // decide_doop / tune_doop: D placement
+    float doop_ms[2] = {-1.f, -1.f};   // tune_doop's Gram-backward times (in place, out of place)
     uint32_t* mu = nullptr; uint32_t* me = nullptr;
     void* chain[2] = {};
     float* bott = nullptr; float* gbott = nullptr;
@@ -265,15 +267,18 @@ static size_t tensor_pad() {
     return (size_t)pad;
 }
 
-// Where the Gram backward writes D (the direct loss gradients of the style-tapped tensors): over E
-// in place (default since round 4: 24.14-24.18 ms in 5 of 5 processes against 25.0-25.1 out of
-// place, B = 256, T = 16384, with the tensor pad and the round-4 kernels; round 2 had measured
-// in place switching between ~23 and ~27 ms per process before the pad), or, ASTYLE_DOOP=1, to a
-// buffer of its own (+1 activation set of memory).
-static bool d_out_of_place() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("ASTYLE_DOOP"); v = e ? (atoi(e) != 0) : 0; }
-    return v != 0;
+// Where the Gram backward writes D (the direct loss gradients of the style-tapped tensors): to a
+// buffer of its own (out of place, +1 activation set of memory) or over E in place.  Round 6 rule
+// (DESIGN.md §2): out of place whenever the workspace with it leaves
+// max(16 GiB, 10 %) of the device's memory free, in place otherwise (B > ~480 clips of 16384 on
+// a 288-GB MI355X).  Out of place ran 23.8-24.1 ms in 9 of 9 processes in round 3, where in place
+// ran 26.8-27.1 ms in 19 of 22 (the DRAM credit stalls of the write-over-read pattern); in round 5
+// one box of five ran every in-place Gram backward at 27.1-27.3 ms; on fast boxes the two modes are
+// within +-0.4 ms (round 5 and 6 A/Bs).  ASTYLE_DOOP=1 / 0 forces either mode (A/B runs).
+static int doop_env() {
+    static int v = -2;
+    if (v == -2) { const char* e = getenv("ASTYLE_DOOP"); v = e ? (atoi(e) != 0) : -1; }
+    return v;
 }
 // Byte offset of the D buffer inside its allocation (ASTYLE_DPAD, A/B of the Gram backward's
 // read / write address interplay; a multiple of 256)
@@ -291,8 +296,8 @@ size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     size_t n = 0;
     n += W_TOTAL * 4 + (size_t)NBLK_MAX * BLKB_SZ * 2;
     if (c->precision == 2) n += (size_t)NBLK_MAX * SBLK * 16 + 2 * (size_t)(NBLK_MAX + 1) * c->batch * 4;
-    n += (size_t)(x->nblk + 1) * (BTC + tensor_pad()) * es * (d_out_of_place() ? 2 : 1);   // act (+ D)
-    if (d_out_of_place()) n += d_pad();
+    n += (size_t)(x->nblk + 1) * (BTC + tensor_pad()) * es * (x->doop ? 2 : 1);   // act (+ D)
+    if (x->doop) n += d_pad();
     n += 2 * (size_t)x->nblk * c->batch * c->T * 16;        // mu, me
     n += 2 * BTC * es;                                      // chain
     int ncg = 0;
@@ -310,6 +315,78 @@ size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     const int nf = stft_frames(c->T);
     if (nf) n += 1024 * 8 + (size_t)c->batch * nf * (1 + 1024) * 4;   // STFT regulariser
     return n;
+}
+
+// the D placement of a context (x->doop) on the current device: forced by ASTYLE_DOOP, else out
+// of place when workspace_bytes with it leaves max(16 GiB, 10 % of the device) free
+static void decide_doop(const ast_cfg* c, ast_ctx* x) {
+    const int env = doop_env();
+    if (env >= 0) { x->doop = env != 0; return; }
+    x->doop = true;
+    const size_t need = workspace_bytes(c, x);
+    x->doop = false;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); return; }
+    const size_t margin = std::max<size_t>((size_t)16 << 30, tot / 10);
+    x->doop = need + margin <= fr;
+}
+
+void launch_gram_bwd_any(ast_ctx* x, const GramArgs& g, hipStream_t s);
+GramArgs gram_args(ast_ctx* x);
+GatysArgs gatys_args(ast_ctx* x);
+
+// Where both placements fit (x->dgrad allocated, D at least 4 GiB) and ASTYLE_DOOP does not force
+// one: time the context's own Gram backward (no content tap, no max) on its own buffers in both
+// placements, twice each (in place, out of place, in place, out of place; best of two), and keep
+// the faster, releasing the D buffer when in place wins (by more than 1 %).  The slow in-place
+// mode depends on the physical pages a process got, so it is measured, not
+// guessed: ~90 ms at B = 256, T = 16384.  Results are bit-identical in both placements.
+static int tune_doop(ast_ctx* x) {
+    if (doop_env() >= 0 || !x->dgrad) return 0;
+    const size_t dbytes = (size_t)(x->nblk + 1) * x->tstride * x->esz;
+    if (dbytes < ((size_t)4 << 30)) return 0;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    float best[2] = {1e30f, 1e30f};
+    for (int rep = 0; rep < 2; ++rep)
+        for (int m = 0; m < 2; ++m) {
+            (void)hipEventRecord(e0, nullptr);
+            if (x->cfg.gatys) {
+                GatysArgs g = gatys_args(x);
+                g.actw = m ? x->dgrad : x->act;
+                launch_gatys_bwd(g, x->split ? 2 : (x->bf ? 1 : 0), nullptr);
+            } else {
+                GramArgs g = gram_args(x);
+                g.actw = m ? x->dgrad : x->act;
+                g.nchunk = x->nchunk_b;
+                launch_gram_bwd_any(x, g, nullptr);
+            }
+            (void)hipEventRecord(e1, nullptr);
+            hipError_t e = hipEventSynchronize(e1);
+            float ms = 0.f;
+            if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+            if (e != hipSuccess) {
+                (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+                return fail(AST_E_HIP, hipGetErrorString(e));
+            }
+            best[m] = std::min(best[m], ms);
+        }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    x->doop_ms[0] = best[0];
+    x->doop_ms[1] = best[1];
+    if (best[0] < 0.99f * best[1]) {   // in place: give the D buffer back
+        void* base = (char*)x->dgrad - d_pad();
+        auto it = std::find(x->allocs.begin(), x->allocs.end(), base);
+        if (it != x->allocs.end()) {
+            (void)hipFree(base);
+            x->allocs.erase(it);
+        }
+        x->dgrad = nullptr;
+        x->doop = false;
+    }
+    return 0;
 }
 
 // ASTYLE_GUARD=1 (diagnostic): every buffer gets a GUARD_BYTES band of GUARD_FILL on both
@@ -626,7 +703,15 @@ int ast_workspace_bytes(const ast_cfg* cfg, size_t* out) {
     tmp.cfg = *cfg;
     int rc = plan(cfg, &tmp);
     if (rc) return rc;
+    decide_doop(cfg, &tmp);   // (the current device's free memory, as ast_create on it decides)
     *out = workspace_bytes(cfg, &tmp);
+    return 0;
+}
+
+int ast_d_out_of_place(const ast_ctx* x, int* out, float* tuned_ms) {
+    if (!x || !out) return fail(AST_E_ARG, "null argument");
+    *out = x->doop ? 1 : 0;
+    if (tuned_ms) { tuned_ms[0] = x->doop_ms[0]; tuned_ms[1] = x->doop_ms[1]; }
     return 0;
 }
 
@@ -639,6 +724,7 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     x->dev = hip_device;
     hipError_t e = hipSetDevice(hip_device);
     if (e != hipSuccess) { delete x; return fail(AST_E_HIP, hipGetErrorString(e)); }
+    decide_doop(cfg, x);
     const ast_cfg& c = *cfg;
     const size_t BTC = (size_t)c.batch * c.T * C;
     x->tstride = BTC + tensor_pad();
@@ -658,7 +744,7 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     ALLOC(x->wtsb, (size_t)NBLK_MAX * BLKB_SZ * 2);
     (void)hipMemset(x->wtsb, 0, (size_t)NBLK_MAX * BLKB_SZ * 2);
     ALLOC(x->act, (size_t)(x->nblk + 1) * x->tstride * x->esz);
-    if (d_out_of_place()) {
+    if (x->doop) {
         ALLOC(x->dgrad, (size_t)(x->nblk + 1) * x->tstride * x->esz + d_pad());
         x->dgrad = (char*)x->dgrad + d_pad();   // (x->allocs keeps the base for hipFree)
     }
@@ -695,6 +781,7 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
         if (e != hipSuccess) { ast_destroy(x); return fail(AST_E_HIP, hipGetErrorString(e)); }
     }
 #undef ALLOC
+    if ((rc = tune_doop(x))) { ast_destroy(x); return rc; }
     *out = x;
     return 0;
 }

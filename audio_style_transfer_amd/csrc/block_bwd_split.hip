@@ -31,6 +31,12 @@
 //      conversion of tile i+1 and, unit by unit behind it, the row loads of tile i+2
 //   D  g_a, column half 1; carries epilogue half 0 of tile i
 // The first tile is peeled so every loop iteration issues the same vector-memory sequence.
+// non-temporal (nt) row loads; the stores keep the default policy: they leave the accumulator
+// layout as 16-B pieces of 32 lines per instruction, which L2 merges into whole lines, and nt made
+// them partial-line writes to DRAM (+75 % per launch, profiles/r6_diag/nt_ab.txt)
+#ifndef SW_BWD_DEFAULT_POLICY
+#define SW_LD_AUX 2
+#endif
 #include "splitwave.h"
 #include <algorithm>
 #include <cstdio>

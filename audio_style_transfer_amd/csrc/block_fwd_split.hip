@@ -24,6 +24,13 @@
 //   D  GEMM 2, half 1; carries the conversion of tile i+1 (image + residual)
 // Round-2 measurements of this structure: ~13k cycles per tile against an MFMA
 // floor of 6.2k; moving the loads / conversions between phases does not change the tile time.
+// non-temporal (gfx950 CPol nt) row loads and e_{l+1} stores: every row streams through once, and
+// the stores are whole 128-B lines (round 6: -1.0 % per launch from the stores, -0.4 % from the
+// loads, profiles/r6_diag/nt_ab.txt); -DSW_FWD_DEFAULT_POLICY (A/B builds) restores the default
+#ifndef SW_FWD_DEFAULT_POLICY
+#define SW_LD_AUX 2
+#define SW_ST_AUX 2
+#endif
 #include "splitwave.h"
 #include <algorithm>
 #include <cstdio>

@@ -158,6 +158,16 @@ class StyleEngine:
         _lib.check(self.lib.ast_set_targets(self.h, self._ptr(phi_c), int(c_shared),
                                             self._ptr(phi_s), int(s_shared)))
 
+    def d_out_of_place(self, with_times: bool = False):
+        """Whether this context keeps the Gram backward's D in a buffer of its own rather than
+        in place over the activations (ast_workspace_bytes' memory-fit rule, then ast_create's
+        timing of both placements); with_times: (flag, (ms in place, ms out of place)), -1 where
+        not timed."""
+        v = ctypes.c_int()
+        ms = (ctypes.c_float * 2)()
+        _lib.check(self.lib.ast_d_out_of_place(self.h, ctypes.byref(v), ctypes.cast(ms, ctypes.c_void_p)))
+        return (bool(v.value), (ms[0], ms[1])) if with_times else bool(v.value)
+
     def set_cu_limit(self, cus: int) -> None:
         """At most ``cus`` CUs for the persistent split block kernels (0 = all): for running
         several engines (disjoint clip groups) concurrently on one GPU, one stream each."""

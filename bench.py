@@ -204,6 +204,8 @@ def run(args, Eng, precision, steps, warmup, ws, rank, dev, graph, clips=None, g
     sync(dev)
     tm = eng.timing_read()
     eng.timing(False)
+    dop = getattr(eng, 'd_out_of_place', None)
+    tm['d_out_of_place'], tm['d_tuned_ms'] = dop(with_times=True) if dop else (None, None)
     del loop, xs
     for e in engs:
         e.close()
@@ -501,6 +503,8 @@ def rank_main(args):
                    'precision': args.precision, 'precision_detail': PREC_NOTE[args.precision],
                    'hip_graph': bool(args.graph),
                    'clip_groups': B // Bt,
+                   'gram_d': {True: 'out of place', False: 'in place', None: None}[tm.get('d_out_of_place')],
+                   'gram_d_tuned_ms': tm.get('d_tuned_ms'),
                    'breakdown_engine_clips': Bt},
         'clip_iters_per_s': value * 256.0,
         'roofline': block_roofline(args.precision, Bt, T, fwd_ms, bwd_ms, traffic,

@@ -1,5 +1,6 @@
 """CPU: libastyle.so loads, exports every symbol include/astyle.h declares, its ast_cfg layout
-matches the header, and host-side validation (ast_workspace_bytes: no HIP calls) behaves."""
+matches the header, and host-side validation (ast_workspace_bytes: no device allocation; the D-placement rule reads
+the free memory, and without a GPU it keeps D in place) behaves."""
 import ctypes
 import os
 import re

@@ -54,3 +54,39 @@ def test_gram_backward_half_rows_equals_quarter_rows(tmp_path):
     assert np.array_equal(a['g0'], b['g0'])
     assert np.allclose(a['p0'], b['p0'], rtol=1e-6, atol=0)
     assert np.array_equal(a['p1'], b['p1']) and np.array_equal(a['g1'], b['g1'])   # (Gatys: not affected)
+
+
+PLACE = r'''
+import os, sys, json, torch
+sys.path.insert(0, sys.argv[1])
+from audio_style_transfer_amd.engine import StyleEngine
+res = {}
+for gatys in (0, 1):
+    # D of 31 x 32 x 16384 x 128 fp32 = 8 GiB: ast_create times both placements
+    e = StyleEngine(32, 16384, [29], list(range(30)), precision='split',
+                    device=torch.device('cuda', 0), lambd=100.0, gatys=bool(gatys))
+    res[gatys] = e.d_out_of_place(with_times=True)
+    e.close()
+small = StyleEngine(1, 4096, [29], list(range(30)), precision='split', device=torch.device('cuda', 0))
+res['small'] = small.d_out_of_place(with_times=True)
+small.close()
+print(json.dumps(res))
+'''
+
+
+def test_default_placement_is_the_timed_faster_one(tmp_path):
+    """Round 6 default (VERDICT r5 next #2): D out of place where it fits, and where both fit and
+    D is >= 4 GiB, ast_create times the context's Gram backward in both placements and keeps the
+    faster (in place only when it wins by > 1 %).  A small context is not timed (out of place)."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k != 'ASTYLE_DOOP'}
+    r = subprocess.run([sys.executable, '-c', PLACE, ROOT], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ('0', '1'):
+        flag, (t_in, t_out) = res[k]
+        assert t_in > 0 and t_out > 0, res
+        assert flag == (not t_in < 0.99 * t_out), res
+    flag, (t_in, t_out) = res['small']
+    assert flag and t_in < 0 and t_out < 0, res
