@@ -429,7 +429,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
     x->lg_front_done = false;   // phase 1's state (act, gmax) is about to be overwritten
     const ast_cfg& c = x->cfg;
     if (x->split) {
-        launch_zero32(x->gmax_e, (size_t)(NBLK_MAX + 1) * c.batch * 4, s);
+        launch_zero32(x->gmax_e, (size_t)(NBLK_MAX + 1) * c.batch * 4, s, 0);
         // e_0 is not stored: block 0 recomputes it from x (FwdArgsS::xin); masks and max only
         launch_startconv_masks((const float*)xd, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s,
                                (uint16_t*)x->me, x->gmax_e);
@@ -1032,7 +1032,7 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
     bool first_bott = true;
     const int fuse_u = fused_content_occ(x);
     if (fuse_u >= 0)   // the Gram backward writes (T / GRAM_CSLOT) x 4 = ncpart partial slots per clip
-        launch_zero32(x->cpart, (size_t)c.batch * x->ncpart * 4, s);
+        launch_zero32(x->cpart, (size_t)c.batch * x->ncpart * 4, s, 1);
     for (size_t i = 0; i < x->occ.size(); ++i) {
         if (fuse_u >= 0) break;
         const Occ& o = x->occ[i];
@@ -1071,7 +1071,7 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
         if (x->split && x->tensor_in_style[x->nblk]) {   // the chain's first max |tot| inside the Gatys bwd
             for (int u = 0; u < x->nu; ++u) if (x->uid[u] == x->nblk) g.top_u = u;
             g.gmax_top = x->gmax_g + (size_t)x->nblk * c.batch;
-            launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s);
+            launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s, 2);
             top_max_done = g.top_u >= 0;
         }
         if (fuse_u >= 0) {   // the split Gatys backward adds the content tap (one slot per 512-row tile)
@@ -1096,7 +1096,7 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
         if (x->split && x->tensor_in_style[x->nblk]) {   // the chain's first max |tot| inside the Gram bwd
             for (int u = 0; u < x->nu; ++u) if (x->uid[u] == x->nblk) g.top_u = u;
             g.gmax_top = x->gmax_g + (size_t)x->nblk * c.batch;
-            launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s);
+            launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s, 2);
             top_max_done = g.top_u >= 0;
         }
         if (fuse_u >= 0) {
@@ -1125,7 +1125,7 @@ static int loss_grad_back(ast_ctx* x, const float* xd, float* grad, float* parts
         return x->tensor_in_style[t] ? (x->dgrad ? (const void*)((char*)x->dgrad + (size_t)t * x->tstride * x->esz) : tens(x, t)) : x->cg_buf[t];
     };
     if (x->split && !top_max_done) {
-        launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s);
+        launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s, 2);
         const void* top = direct(x->nblk);
         if (!top) return fail(AST_E_STATE, "top block has no loss gradient");
         launch_absmax((const float*)top, (size_t)c.T * C, c.batch, x->gmax_g + (size_t)x->nblk * c.batch, s);
@@ -1257,7 +1257,7 @@ int ast_set_cu_limit(ast_ctx* x, int cus) {
 
 int ast_range_flags_reset(ast_ctx* x, void* stream) {
     if (!x) return fail(AST_E_ARG, "null argument");
-    launch_zero32(x->rflags, (size_t)x->cfg.batch * 4, S(stream));
+    launch_zero32(x->rflags, (size_t)x->cfg.batch * 4, S(stream), 3);
     return 0;
 }
 
@@ -1299,7 +1299,7 @@ int ast_lbfgs_begin(ast_ctx* x, void* ws, float* xd, const double* x0, const int
         return fail(AST_E_STATE, "continuing (x0 NULL) needs a workspace started with x0");
     if (x0 && !known) x->lb_ws.push_back(ws);
     // a new epoch: the range flags accumulate over its evaluations (include/astyle.h)
-    launch_zero32(x->rflags, (size_t)x->cfg.batch * 4, S(stream));
+    launch_zero32(x->rflags, (size_t)x->cfg.batch * 4, S(stream), 3);
     launch_lbfgs_begin(ws, xd, x0, active, x->cfg.batch, x->cfg.T, m, maxiter, maxls, ftol, gtol,
                        S(stream));
     HIPCHK(hipGetLastError());

@@ -314,7 +314,9 @@ void launch_startconv_fwd(const float* x, S* e0, const float* w0, const float* b
 void launch_startconv_masks(const float* x, const float* w0, const float* b0, int B, int T,
                             hipStream_t s, uint16_t* me0, unsigned* gmax);
 void launch_startx_gx(const float* spart, float* gx, int B, int T, hipStream_t s);
-void launch_zero32(void* p, size_t bytes, hipStream_t s);   // bytes: a multiple of 4
+// bytes: a multiple of 4; site: which clear (0 gmax_e, 1 content partials, 2 gmax_g, 3 range
+// flags), used only by the tools-only memset build's per-site selection (ASTYLE_MEMSET_SITES)
+void launch_zero32(void* p, size_t bytes, hipStream_t s, int site = -1);
 template <typename S>
 void launch_startconv_bwd(const S* g0, float* gx, const float* w0, int B, int T,
                           hipStream_t s);

@@ -536,14 +536,19 @@ void launch_bottleneck_bwd(const float* gy, S* ge, const float* wb, int accumula
 __global__ void __launch_bounds__(256) k_zero32(uint32_t* __restrict__ p, size_t n) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) p[i] = 0u;
 }
-void launch_zero32(void* p, size_t bytes, hipStream_t s) {
+void launch_zero32(void* p, size_t bytes, hipStream_t s, int site) {
     const size_t n = bytes / 4;
     if (!n) return;
 #ifdef ASTYLE_MEMSET_CLEARS
     // tools-only build (ASTYLE_VARIANT=memset ASTYLE_DEFS=-DASTYLE_MEMSET_CLEARS): the round-4
-    // hipMemsetAsync clears, for tools/determinism2.py (graph replays)
-    (void)hipMemsetAsync(p, 0, bytes, s);
-    return;
+    // hipMemsetAsync clears, for tools/determinism2.py (graph replays); env
+    // ASTYLE_MEMSET_SITES=<bit mask of sites> keeps the other sites on k_zero32 (default: all)
+    static int mask = -1;
+    if (mask < 0) { const char* e = getenv("ASTYLE_MEMSET_SITES"); mask = e ? atoi(e) : 0xff; }
+    if (site < 0 || ((mask >> site) & 1)) {
+        (void)hipMemsetAsync(p, 0, bytes, s);
+        return;
+    }
 #endif
     const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
     hipLaunchKernelGGL(k_zero32, dim3(blocks), dim3(256), 0, s, (uint32_t*)p, n);
