@@ -11,15 +11,14 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, 'csrc')
 LIB = os.path.join(PKG, 'libastyle.so')
 SOURCES = ['encoder.hip', 'block_fwd_bf16.hip', 'block_bwd_bf16.hip', 'block_fwd_split.hip',
-           'block_bwd_split.hip', 'gram.hip', 'gram_bf16.hip', 'gram_split.hip', 'gram_gatys.hip',
+           'block_bwd_split.hip', 'block_fwd_split16.hip', 'block_bwd_split16.hip', 'gram.hip', 'gram_bf16.hip', 'gram_split.hip', 'gram_gatys.hip',
            'stft_reg.hip', 'lbfgs.hip', 'ot_admm.hip', 'api.hip', 'ckpt.cpp']
-# tools-only A/B build (ASTYLE_VARIANT=fwdvariants -> libastyle_fwdvariants.so): the measured-
-# slower forward block kernels of round 3, selected at run time by
-# ASTYLE_FWD_ROLES=1 / ASTYLE_FWD_DB=1; never part of the shipped libastyle.so
+# tools-only A/B builds (ASTYLE_VARIANT=<name> [ASTYLE_DEFS=...] -> libastyle_<name>.so) may add
+# sources from tools/variants here; round 6 retired the round-3/4 alternative forward kernels
+# (role split, double-buffered image, Winograd timing probes: written for the 32x32x16 fragment
+# layout, measured slower)
 VARIANTS = os.path.join(os.path.dirname(PKG), 'tools', 'variants')
-VARIANT_SOURCES = {'fwdvariants': (['block_fwd_roles.hip', 'block_fwd_db.hip', 'block_fwd_winoprobe.hip',
-                                    'block_bwd_winoprobe.hip'],
-                                   ['-DASTYLE_FWD_VARIANTS'])}
+VARIANT_SOURCES = {}
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 CXX = os.environ.get('CXX', 'g++')          # host-only sources (.cpp)
 CXXFLAGS = ['-O2', '-fPIC', '-std=c++17', '-Wall']
@@ -33,8 +32,7 @@ _CW = ['-mllvm', '-amdgpu-mfma-vgpr-form=1', '-mllvm', '-amdgpu-atomic-optimizer
 if os.environ.get('ASTYLE_NO_VGPR_FORM'):   # A/B builds: let the compiler place MFMA accumulators (AGPRs)
     _CW = _CW[2:]
 EXTRA = {'block_fwd_bf16.hip': _CW, 'block_bwd_bf16.hip': _CW, 'block_fwd_split.hip': _CW,
-         'block_bwd_split.hip': _CW, 'block_fwd_roles.hip': _CW, 'block_fwd_db.hip': _CW,
-         'block_fwd_winoprobe.hip': _CW, 'block_bwd_winoprobe.hip': _CW}
+         'block_bwd_split.hip': _CW, 'block_fwd_split16.hip': _CW, 'block_bwd_split16.hip': _CW}
 
 
 def _stale(lib: str = LIB, extra=()) -> bool:
@@ -47,9 +45,9 @@ def _stale(lib: str = LIB, extra=()) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_variant(name: str = 'fwdvariants', force: bool = False) -> str:
+def build_variant(name: str, force: bool = False) -> str:
     """The tools-only A/B library libastyle_<name>.so of VARIANT_SOURCES[name], rebuilt from the
-    committed sources whenever they changed (tests/test_gpu_roles.py loads it)."""
+    committed sources whenever they changed."""
     lib = os.path.join(PKG, 'libastyle_%s.so' % name)
     extra = [os.path.join(VARIANTS, f) for f in VARIANT_SOURCES.get(name, ([], []))[0]]
     if not force and not _stale(lib, extra):

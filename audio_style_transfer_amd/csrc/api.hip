@@ -290,6 +290,27 @@ static size_t d_pad() {
 
 int fused_content_occ(const ast_ctx* x);
 
+// ASTYLE_MFMA16=1: the split block kernels on v_mfma_f32_16x16x32_f16 (block_*_split16.hip,
+// round 6: measured no faster); read once per process, since the weight fragments
+// are packed for the kernels that will read them
+static bool mfma16_on() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("ASTYLE_MFMA16"); v = e && atoi(e) ? 1 : 0; }
+    return v == 1;
+}
+// (K index kk, output-channel index mm) of element e of lane ln in fragment slot kb of wave w
+// (common.h: the split weight layouts)
+static void frag_index(int kb, int ln, int e, int w, int& kk, int& mm) {
+    if (mfma16_on()) {
+        const int ii = ln & 15, qq = ln >> 4;
+        kk = 32 * (kb >> 1) + 8 * qq + e;
+        mm = 32 * w + 16 * (kb & 1) + ii;
+    } else {
+        kk = 16 * kb + 8 * (ln >> 5) + e;
+        mm = 32 * w + (ln & 31);
+    }
+}
+
 size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     const size_t BTC = (size_t)c->batch * c->T * C;
     const size_t es = c->precision == 1 ? 2 : 4;
@@ -458,7 +479,8 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
             a.wdn = x->wdn[l]; a.bdm = x->bdm[l];
             a.cus = x->cus;
             a.xin = l == 0 ? xd : nullptr; a.w0 = x->wts + W0_OFF; a.b0 = x->wts + B0_OFF;
-            launch_block_fwd_s(a, s);
+            if (mfma16_on()) launch_block_fwd_s16(a, s);
+            else launch_block_fwd_s(a, s);
         } else if (x->bf) {
             FwdArgsC a;
             a.stamps = g_stamps;
@@ -842,7 +864,7 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
             HIPCHK(hipMemcpy(dst + WBFB, hg.data(), 3 * C * C * 2, hipMemcpyHostToDevice));
             if (x->split) {
                 // forward: element (w, tap, kb, hl, lane (m, h), e) = W_d[tap][16 kb + 8 h + e][32 w + m];
-                // backward: W_d[tap][32 w + m][16 kb + 8 h + e]
+                // backward: W_d[tap][32 w + m][16 kb + 8 h + e] (ASTYLE_MFMA16: frag_index)
                 const int k = weight_exp(host, 3 * C * C);
                 x->kd[l - 1] = k;
                 float nrm = 0.f;
@@ -858,8 +880,8 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                         for (int kb = 0; kb < 8; ++kb)
                             for (int ln = 0; ln < 64; ++ln)
                                 for (int e = 0; e < 8; ++e) {
-                                    const int m = ln & 31, hh = ln >> 5;
-                                    const int kk = 16 * kb + 8 * hh + e, mm = 32 * w + m;
+                                    int kk, mm;
+                                    frag_index(kb, ln, e, w, kk, mm);
                                     const size_t o = ((((size_t)(w * 3 + tp) * 8 + kb) * 2) * 64 + ln) * 8 + e;
                                     split_half(host[(size_t)tp * C * C + kk * C + mm], k, f[o], f[o + 64 * 8]);
                                     split_half(host[(size_t)tp * C * C + mm * C + kk], k, g[o], g[o + 64 * 8]);
@@ -904,7 +926,7 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
             HIPCHK(hipMemcpy(dst + WRBFB, hg.data(), C * C * 2, hipMemcpyHostToDevice));
             if (x->split) {
                 // forward: element (w, kb, hl, lane (m, h), e) = W_r[16 kb + 8 h + e][32 w + m];
-                // backward: W_r[32 w + m][16 kb + 8 h + e]
+                // backward: W_r[32 w + m][16 kb + 8 h + e] (ASTYLE_MFMA16: frag_index)
                 const int k = weight_exp(host, C * C);
                 x->kr[l - 1] = k;
                 float nrm = 0.f;
@@ -919,8 +941,8 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                     for (int kb = 0; kb < 8; ++kb)
                         for (int ln = 0; ln < 64; ++ln)
                             for (int e = 0; e < 8; ++e) {
-                                const int m = ln & 31, hh = ln >> 5;
-                                const int kk = 16 * kb + 8 * hh + e, mm = 32 * w + m;
+                                int kk, mm;
+                                frag_index(kb, ln, e, w, kk, mm);
                                 const size_t o = ((((size_t)w * 8 + kb) * 2) * 64 + ln) * 8 + e;
                                 split_half(host[(size_t)kk * C + mm], k, f[o], f[o + 64 * 8]);
                                 split_half(host[(size_t)mm * C + kk], k, g[o], g[o + 64 * 8]);
@@ -1158,7 +1180,8 @@ static int loss_grad_back(ast_ctx* x, const float* xd, float* grad, float* parts
             // block 0: the start conv's backward folded in; chain[0] holds the wave partials
             a.w0 = x->wts + W0_OFF;
             a.spart = l == 0 ? (float*)x->chain[0] : nullptr;
-            launch_block_bwd_s(a, s);
+            if (mfma16_on()) launch_block_bwd_s16(a, s);
+            else launch_block_bwd_s(a, s);
         } else if (x->bf) {
             // the bf16 chain holds d loss / d e_l with D_l already added (the kernel adds it)
             BwdArgsC a;

@@ -33,7 +33,7 @@
 // The first tile is peeled so every loop iteration issues the same vector-memory sequence.
 // non-temporal (nt) row loads; the stores keep the default policy: they leave the accumulator
 // layout as 16-B pieces of 32 lines per instruction, which L2 merges into whole lines, and nt made
-// them partial-line writes to DRAM (+75 % per launch, profiles/r6_diag/nt_ab.txt)
+// them partial-line writes to DRAM (+75 % per launch, profiles/r6_diag/block_ab.txt)
 #ifndef SW_BWD_DEFAULT_POLICY
 #define SW_LD_AUX 2
 #endif
@@ -60,7 +60,11 @@ constexpr int LA = 2;                 // B-fragment lookahead (steps)
 // halo rows (p0 - 1, p0 + 64) are SAME padding, so the column tiles cover p0 .. p0 + 63 and rows
 // 0 / 65 of the g_u image stay zero: no halo MFMA tile
 template <bool MASKED, bool ONESEG, bool HAS_D, bool SX, bool WHOLE>
-__global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout ly) {
+__global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout) {
+    // the layout as compile-time constants (pick_layout: one segment or masked: M = 64 with two
+    // halo rows; else segments of SEGM = 32 with their pad rows), not the launch argument
+    constexpr bool GEO1 = ONESEG || MASKED;
+    const Layout ly = {GEO1 ? TMS : SEGM, GEO1 ? TMS + 2 : (TMS / SEGM) * (SEGM + 2)};
     static_assert(!WHOLE || (ONESEG && !MASKED), "WHOLE is a one-segment layout");
     __shared__ __attribute__((aligned(16))) uint8_t XS[ISLOT];        // split tot image
     __shared__ __attribute__((aligned(16))) uint8_t XG[GROWS * RS];   // split g_u image
@@ -489,14 +493,7 @@ __global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, siz
 
 }  // namespace
 
-#ifdef ASTYLE_FWD_VARIANTS
-bool launch_block_bwd_winoprobe(const BwdArgsS& a, hipStream_t s);   // tools/variants/block_bwd_winoprobe.hip
-#endif
-
 void launch_block_bwd_s(const BwdArgsS& a0, hipStream_t s) {
-#ifdef ASTYLE_FWD_VARIANTS
-    { const char* e = getenv("ASTYLE_BWD_WINOPROBE"); if (e && atoi(e)) { launch_block_bwd_winoprobe(a0, s); return; } }
-#endif
     BwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
     a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));

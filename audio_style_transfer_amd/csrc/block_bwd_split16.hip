@@ -1,9 +1,9 @@
-// TIMING PROBE (tools-only variant, results WRONG by design): the cost structure a Winograd
-// F(2,3) g_a (the transposed dilated conv) would have inside this kernel's budget -- g_a runs two
-// of the three tap groups (96 instead of 144 MFMAs per tile), every g_u image write is followed
-// by a second split of a transformed pair into the row's pad bytes, and the epilogue adds the
-// output transform's two adds per value.  An upper bound of Winograd's gain in the backward
-// (DESIGN.md §3).  ASTYLE_BWD_WINOPROBE=1 in the libastyle_fwdvariants.so build.
+// ASTYLE_MFMA16=1 (round 6): the backward block kernel of block_bwd_split.hip on
+// v_mfma_f32_16x16x32_f16 fragments (splitwave.h "16x16x32"; the weights are packed for it when the
+// knob is set).  Same structure, phases and numerics class; the K accumulation order differs, so
+// results match the default kernels to fp32 rounding, not bit for bit.  Measured (DESIGN.md §3,
+// round 6): as fast as the 32x32x16 default (within 0.3 %) at equal data; kept as the
+// measured alternative, not the default.
 //
 // Split-fp16 encoder block backward (precision 2): d loss / d e_l for one block of
 // model.py:95-116, restated by oracle/astyle_oracle.py:171-189 (encoder_backward):
@@ -12,8 +12,8 @@
 //   g_a = sum_k W_d[k] g_u(p - k + 1)                K = 3 SAME dilated conv transposed, in
 //                                                    time_to_batch positions (masked.py:110-160)
 //   out = tot + D_l + [e_l > 0] g_a                  D_l: direct loss gradient of e_l, if tapped
-// fp32 storage, split fp16 operands on v_mfma_f32_32x32x16_f16, fp32 accumulation and
-// epilogue (splitwave.h).
+// fp32 storage, split fp16 operands on v_mfma_f32_16x16x32_f16 (round 6; 32x32x16 before), fp32
+// accumulation and epilogue (splitwave.h).
 //
 // One workgroup per CU (wave w owns channels 32 w .. 32 w + 31), persistent over tiles of 64
 // positions, one wave per SIMD; the structure of the forward (block_fwd_split.hip): a tile's
@@ -29,11 +29,21 @@
 //   H  (one-segment layouts, unless the workgroup's previous tile is the left neighbour: then
 //      its g_u rows 64 / 65 are copied to rows 0 / 1) g_v of rows 0 / 1 (positions p0 - 1, p0;
 //      the column tiles cover p0 + 1 .. p0 + 64); carries g_u of half 1; g_u of the last column
-//      tile; barrier (g_u image complete, tot image free)
+//      tile; barrier (g_u image complete, tot image free).  The left neighbour includes the
+//      last tile of the previous sub-sequence (CARRY): that tile's right-halo column (p0 + 64,
+//      SAME padding for its own g_a) is computed on the next sub-sequence's first position
+//      instead of a zero row and set aside in g_u row 67, so the next tile's rows 0 / 1 are
+//      (0, row 67) and no tile of a walk pays the halo MFMAs but its first
 //   C  g_a, column half 0 (3 taps x 8 k-steps x 3 products over the g_u image); carries the
 //      conversion of tile i+1 and, unit by unit behind it, the row loads of tile i+2
 //   D  g_a, column half 1; carries epilogue half 0 of tile i
 // The first tile is peeled so every loop iteration issues the same vector-memory sequence.
+// non-temporal (nt) row loads; the stores keep the default policy: they leave the accumulator
+// layout as 16-B pieces of 32 lines per instruction, which L2 merges into whole lines, and nt made
+// them partial-line writes to DRAM (+75 % per launch, profiles/r6_diag/block_ab.txt)
+#ifndef SW_BWD_DEFAULT_POLICY
+#define SW_LD_AUX 2
+#endif
 #include "splitwave.h"
 #include <algorithm>
 #include <cstdio>
@@ -53,8 +63,16 @@ constexpr int LA = 2;                 // B-fragment lookahead (steps)
 // epilogue -- out = d loss / d e_0 is not stored; per position the wave's three dot products
 // sum_c W0[k][c] out[t][c] over its 32 channels go to spart (launch_startx_gx sums the four
 // waves and forms d loss / d x): no 2 GiB g_0 round trip (model.py:82-93)
-template <bool MASKED, bool ONESEG, bool HAS_D, bool SX>
-__global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
+// WHOLE (one-segment layout with n == 64: every tile is a whole sub-sequence, d = T / 64): both
+// halo rows (p0 - 1, p0 + 64) are SAME padding, so the column tiles cover p0 .. p0 + 63 and rows
+// 0 / 65 of the g_u image stay zero: no halo MFMA tile
+template <bool MASKED, bool ONESEG, bool HAS_D, bool SX, bool WHOLE>
+__global__ void __launch_bounds__(FT, 1) k_block_bwd_s16(BwdArgsS a, Layout) {
+    // the layout as compile-time constants (pick_layout: one segment or masked: M = 64 with two
+    // halo rows; else segments of SEGM = 32 with their pad rows), not the launch argument
+    constexpr bool GEO1 = ONESEG || MASKED;
+    const Layout ly = {GEO1 ? TMS : SEGM, GEO1 ? TMS + 2 : (TMS / SEGM) * (SEGM + 2)};
+    static_assert(!WHOLE || (ONESEG && !MASKED), "WHOLE is a one-segment layout");
     __shared__ __attribute__((aligned(16))) uint8_t XS[ISLOT];        // split tot image
     __shared__ __attribute__((aligned(16))) uint8_t XG[GROWS * RS];   // split g_u image
     __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];     // fp32 tot + D_l rows
@@ -64,12 +82,20 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
     const int ntiles = a.B * tiles;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int r = lane & 31, h = lane >> 5;
+    const int i16 = lane & 15, q4 = lane >> 4;   // 16x16x32 fragment lane (splitwave.h)
     const int G = (int)gridDim.x;
     STAMP_DECL
 
     auto tile_of = [&](int tl) { return tile_at<MASKED>(tl, a.ft, a.fn, a.d, ly); };
     auto clampt = [&](int tl) { return tl < ntiles ? tl : ntiles - 1; };
+#ifdef ASTYLE_DIAG_BWD_L2ROWS
+    // diagnostic build only (tools): every row load and store addresses the workgroup's first
+    // tile, so the same instruction stream runs from L2 instead of HBM (results wrong)
+    const Tile t0f = tile_of(blockIdx.x);
+    auto memt = [&](const Tile& t) { (void)t; return t0f; };
+#else
+    auto memt = [&](const Tile& t) { return t; };
+#endif
 
     // this wave's split weight halves (A: rows = channels 32 w.., K = the other side's channels)
     uint4 wr[8][2], wd[3][8][2];
@@ -91,28 +117,39 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
     if (SX)   // (read after the first tile's T barrier)
         for (int i = tid; i < 3 * C; i += FT) W0S[i] = a.w0[i];
 
-    int Lc[2], toff[2];
+    // image row and time offset of the lane's column 16 cb + i16 of column half j
+    int Lc[2][2], toff[2][2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        Lc[j] = frow(32 * j + r, ly);
-        toff[j] = MASKED ? 0 : row_toff(Lc[j], ly, a.d);
-    }
-    const int chb = 32 * w + 4 * h;
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+            Lc[j][cb] = frow(32 * j + 16 * cb + i16, ly);
+            toff[j][cb] = MASKED ? 0 : row_toff(Lc[j][cb], ly, a.d);
+        }
+    const int chq = 32 * w + 4 * q4;  // first channel of this lane's sub-tiles (+ 16 rb)
+    const int mg0 = q4 >> 1;          // mask group of row block 0 (mgrp: + 2 rb); word h = q4 & 1
+    const int mwo = 4 * (q4 & 1) + w; // the lane's word of a position's 8 mask words
     auto ctime = [&](const Tile& t, int cc, int to) { return col_time<MASKED>(t, cc, to, a.fn, a.d); };
     // g_v / g_u rows.  One-segment layouts shift the two column tiles by one row: they cover
     // image rows 2..65 (positions p0 + 1 .. p0 + 64, the right halo included), and rows 0 / 1
     // (p0 - 1, p0) are either the previous tile's rows 64 / 65 (the workgroup's previous tile is
     // the left neighbour in the same sub-sequence: copied, no MFMAs) or the halo tile's
-    // (lane r == 0 -> row 0, r == 1 -> row 1; lanes r >= 2 compute a copy of row 0 and write it
-    // to unused row 66).  Other layouts: the tile's columns, no halo rows.
+    // (one column block: lane i16 == 0 -> row 0, i16 == 1 -> row 1; lanes i16 >= 2 compute a copy
+    // of row 0 and write it to unused row 66).  Other layouts: the tile's columns, no halo rows.
     // masked layouts have the one-segment geometry (row L = position p0 + L - 1, gathered) and
     // a tile may start / end inside a sub-sequence: the same halo rows, tap masks in g_a
-    constexpr bool HALO = ONESEG || MASKED;
-    int Lv[2];
+    constexpr bool HALO = (ONESEG && !WHOLE) || MASKED;
+    // CARRY tiles: the last tile of a sub-sequence with a next position in the clip (p0 + 64,
+    // the next sub-sequence's first position, time q + 1)
+    constexpr bool CARRY = ONESEG && !WHOLE && !MASKED;
+    auto carry_of = [&](const Tile& t) { return CARRY && t.m0 + TMS >= a.n && t.p0 + TMS < a.T; };
+    int Lv[2][2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) Lv[j] = HALO ? Lc[j] + 1 : Lc[j];
-    const int Lh = r == 1 ? 1 : 0;
-    const int Lhw = r < 2 ? Lh : TMS + 2;
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) Lv[j][cb] = HALO ? Lc[j][cb] + 1 : Lc[j][cb];
+    const int Lh = i16 == 1 ? 1 : 0;
+    const int Lhw = i16 < 2 ? Lh : TMS + 2;
 
     // ---- rows of the next tile: tot (-> split image) and D_l (-> residual) ----
     RowUnits<MASKED, ONESEG> ru;
@@ -120,16 +157,28 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
     float4 lt[NU], lg[NU];
     // unmasked layouts load through buffer resources of the tile (rs_t / rs_d, set with the tile)
     rsrc_t rs_t, rs_d;
-    auto set_rs = [&](const Tile& t) {
+    auto set_rs = [&](const Tile& t_) {
+        const Tile t = memt(t_);
         if (!MASKED) {
             rs_t = ru.rsrc_of(a.tin, t, a.T, a.d);
             if (HAS_D) rs_d = ru.rsrc_of(a.dadd, t, a.T, a.d);
         }
     };
-    auto load_unit = [&](const Tile& t, int k) {
+    auto load_unit = [&](const Tile& t_, int k) {
+        const Tile t = memt(t_);
         if (MASKED) {
             lt[k] = ru.load(a.tin, t, k, a.T, a.fn, a.d);
             if (HAS_D) lg[k] = ru.load(a.dadd, t, k, a.T, a.fn, a.d);
+        } else if (CARRY && k == NU - 1) {
+            // unit 8 by 64-bit address: in a CARRY tile the lanes of row 65 (lr == 1) read the
+            // next sub-sequence's first tot row (its D row stays the dummy: row 65's residual is
+            // no output)
+            const int q = t.tb - t.m0 * a.d;
+            const float* pn = a.tin + ((size_t)t.b * a.T + q + 1) * C + ru.cq;
+            const float* pr = reinterpret_cast<const float*>(
+                reinterpret_cast<const char*>(a.tin + ((ptrdiff_t)t.b * a.T + t.tb - a.d) * C) + ru.unit_off(t, k, a.fn));
+            lt[k] = *reinterpret_cast<const float4*>(carry_of(t) && ru.lr == 1 ? pn : pr);
+            if (HAS_D) lg[k] = ru.loadb(rs_d, t, k, a.fn);
         } else {
             lt[k] = ru.loadb(rs_t, t, k, a.fn);
             if (HAS_D) lg[k] = ru.loadb(rs_d, t, k, a.fn);
@@ -148,158 +197,198 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
         *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
         *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
     };
+    // zero bits of a tile's units: a CARRY tile's row 65 is real
+    auto zbits = [&](const Tile& t) {
+        uint32_t z = ru.zero_bits(t, a.fn);
+        if (carry_of(t) && ru.lr == 1) z &= ~(1u << (NU - 1));
+        return z;
+    };
     // ---- relu-mask words (u16, position-indexed): u > 0 of the tile's columns and halos,
     //      e_l > 0 of its columns ----
-    uint32_t mu_c[2], muh_c = 0, me_c[2], mu_n[2], muh_n = 0, me_n[2], me_p = 0;
-    auto load_masks = [&](const Tile& t, uint32_t (&mu)[2], uint32_t& muh, uint32_t (&me)[2]) {
-        const size_t cb = (size_t)t.b * a.T + t.p0;
+    //      (per column half j and column block cb: the lane's word of its column)
+    uint32_t mu_c[2][2], muh_c = 0, me_c[2][2], mu_n[2][2], muh_n = 0, me_n[2][2], me_p[2] = {0u, 0u};
+    auto load_masks = [&](const Tile& t, uint32_t (&mu)[2][2], uint32_t& muh, uint32_t (&me)[2][2]) {
+        const size_t pb = (size_t)t.b * a.T + t.p0;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            // u > 0 of the g_v rows Lv[j]; a position past the clip reads any word (its tot row
-            // is zero)
-            const int pv = HALO ? min(t.p0 + 1 + 32 * j + r, a.T - 1) : t.p0 + 32 * j + r;
-            mu[j] = a.mu[((size_t)t.b * a.T + pv) * 8 + 4 * h + w];
-            me[j] = a.me[(cb + 32 * j + r) * 8 + 4 * h + w];
-        }
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+                // u > 0 of the g_v rows Lv[j][cb]; a position past the clip reads any word (its
+                // tot row is zero)
+                const int c = 32 * j + 16 * cb + i16;
+                const int pv = HALO ? min(t.p0 + 1 + c, a.T - 1) : t.p0 + c;
+                mu[j][cb] = a.mu[((size_t)t.b * a.T + pv) * 8 + mwo];
+                me[j][cb] = a.me[(pb + c) * 8 + mwo];
+            }
         if (HALO) {     // rows 0 / 1: p0 - 1 (outside the clip at p0 == 0: its tot row is zero or tap-masked), p0
-            const int p = t.p0 + (r == 1 ? 0 : -1);
-            muh = a.mu[((size_t)t.b * a.T + (p < 0 ? 0 : p)) * 8 + 4 * h + w];
+            const int p = t.p0 + (i16 == 1 ? 0 : -1);
+            muh = a.mu[((size_t)t.b * a.T + (p < 0 ? 0 : p)) * 8 + mwo];
         }
     };
 
-    // ---- step 1: g_v of column tile J (0, 1; 2 = the halo columns) ----
-    f32x16 acc1[3];
+    // ---- step 1: g_v of column half J (0, 1; 2 = the halo columns: column block 0 only).  Step
+    //      st = (K block st >> 1 of 32, column block st & 1); the halo GEMM's 4 steps carry two
+    //      side slots each ----
+    f32x4 acc1[3][4];
     auto gemm1 = [&](auto j_tag, auto side) {
         constexpr int J = decltype(j_tag)::value;
-        const int row = J < 2 ? Lv[J] : Lh;
+        constexpr int NS = J < 2 ? 8 : 4;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc1[J][i] = 0.f;
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc1[J][n][i] = 0.f;
         uint4 bh[LA + 1], bl[LA + 1];
-        auto bread = [&](int kb, uint4& xh, uint4& xl) {
-            const uint8_t* p = XS + row * RS + kb * 32 + h * 16;
+        auto bread = [&](int st, uint4& xh, uint4& xl) {
+            const int kb = J < 2 ? st >> 1 : st, cb = J < 2 ? st & 1 : 0;
+            const int row = J < 2 ? Lv[J < 2 ? J : 0][cb] : Lh;
+            const uint8_t* p = XS + row * RS + kb * 64 + q4 * 16;
             xh = lds16(p);
             xl = lds16(p + 256);
         };
 #pragma unroll
         for (int q = 0; q < LA; ++q) bread(q, bh[q], bl[q]);
 #pragma unroll
-        for (int kb = 0; kb < 8; ++kb) {
-            const int cb = kb % (LA + 1);
-            acc1[J] = mfma_f16(wr[kb][0], bh[cb], acc1[J]);
-            if (kb + LA < 8) bread(kb + LA, bh[(kb + LA) % (LA + 1)], bl[(kb + LA) % (LA + 1)]);
-            side(kb);
-            acc1[J] = mfma_f16(wr[kb][1], bh[cb], acc1[J]);
-            acc1[J] = mfma_f16(wr[kb][0], bl[cb], acc1[J]);
-            step3_schedule();
+        for (int st = 0; st < NS; ++st) {
+            const int kb = J < 2 ? st >> 1 : st, cb = J < 2 ? st & 1 : 0, bi = st % (LA + 1);
+            f32x4& c0 = acc1[J][2 * cb];
+            f32x4& c1 = acc1[J][2 * cb + 1];
+            c0 = mfma16(wr[2 * kb][0], bh[bi], c0);
+            c1 = mfma16(wr[2 * kb + 1][0], bh[bi], c1);
+            if (st + LA < NS) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
+            if (J < 2) side(st);
+            else { side(2 * st); side(2 * st + 1); }
+            c0 = mfma16(wr[2 * kb][1], bh[bi], c0);
+            c1 = mfma16(wr[2 * kb + 1][1], bh[bi], c1);
+            c0 = mfma16(wr[2 * kb][0], bl[bi], c0);
+            c1 = mfma16(wr[2 * kb + 1][0], bl[bi], c1);
+            step6_schedule();
         }
     };
-    // g_u unit (J, g) in two parts: mask; scale + split -> image row
+    // g_u of sub-tile (J, g) (rb = g & 1, cb = g >> 1; the halo tile: g < 2) in two parts: mask;
+    // scale + split -> image row
     float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
+    int Lv1t[2] = {Lv[1][0], Lv[1][1]};   // rows of half 1 (a CARRY tile: its right-halo column 63 -> row 67)
     auto gu_part = [&](int J, int g, int part, float f) {
+        const int rb = g & 1, cb = g >> 1;
         if (part == 0) {
-            const uint32_t wd_ = J < 2 ? mu_c[J] : muh_c;
-            gq.x = keep_if(acc1[J][4 * g + 0], wd_, g);
-            gq.y = keep_if(acc1[J][4 * g + 1], wd_, 4 + g);
-            gq.z = keep_if(acc1[J][4 * g + 2], wd_, 8 + g);
-            gq.w = keep_if(acc1[J][4 * g + 3], wd_, 12 + g);
+            const uint32_t wd_ = J < 2 ? mu_c[J < 2 ? J : 0][cb] : muh_c;
+            const int mg = mg0 + 2 * rb;
+            gq.x = keep_if(acc1[J][g][0], wd_, mg);
+            gq.y = keep_if(acc1[J][g][1], wd_, 4 + mg);
+            gq.z = keep_if(acc1[J][g][2], wd_, 8 + mg);
+            gq.w = keep_if(acc1[J][g][3], wd_, 12 + mg);
         } else {
             // the scale after the mask (f is a power of two: the same values), so that the
             // split's low half fuses with it into one v_fma_mix_f32
             uint32_t h01, l01, h23, l23;
             split2s(gq.x * f, gq.y * f, h01, l01);
             split2s(gq.z * f, gq.w * f, h23, l23);
-            uint8_t* p = XG + (J < 2 ? Lv[J] : Lhw) * RS + 2 * (chb + 8 * g);
+            uint8_t* p = XG + (J == 0 ? Lv[0][cb] : J == 1 ? Lv1t[cb] : Lhw) * RS + 2 * (chq + 16 * rb);
             *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
             *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
-            {   // (probe) a transformed pair's add + split into the row's pad bytes
-                uint32_t g01, m01, g23, m23;
-                split2s((gq.x + gq.y) * f, (gq.y - gq.x) * f, g01, m01);
-                split2s((gq.z + gq.w) * f, (gq.w - gq.z) * f, g23, m23);
-                *reinterpret_cast<uint2*>(XG + (J < 2 ? Lv[J] : Lhw) * RS + 512) = make_uint2(g01 ^ m01, g23 ^ m23);
-            }
         }
     };
 
-    // ---- step 2: g_a of column half J ----
-    f32x16 acc2[2];
+    // ---- step 2: g_a of column half J; step st = (tap st >> 3, K block (st & 7) >> 1, column
+    //      block st & 1) ----
+    f32x4 acc2[2][4];
     auto gemm2 = [&](auto j_tag, auto side, const Tile& cu) {
         constexpr int J = decltype(j_tag)::value;
-        bool ok0 = true, ok2 = true;
+        bool ok0[2] = {true, true}, ok2[2] = {true, true};
         if (MASKED) {
-            const int pc = cu.p0 + 32 * J + r;
-            const int m = pc - (int)fdiv((uint32_t)pc, a.fn) * a.n;
-            ok0 = m > 0;
-            ok2 = m < a.n - 1;
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+                const int pc = cu.p0 + 32 * J + 16 * cb + i16;
+                const int m = pc - (int)fdiv((uint32_t)pc, a.fn) * a.n;
+                ok0[cb] = m > 0;
+                ok2[cb] = m < a.n - 1;
+            }
         }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc2[J][i] = 0.f;
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc2[J][n][i] = 0.f;
         uint4 bh[LA + 1], bl[LA + 1];
         auto bread = [&](int st, uint4& xh, uint4& xl) {
-            const int tp = st >> 3, kb = st & 7;
-            const uint8_t* p = XG + (Lc[J] + 1 - tp) * RS + kb * 32 + h * 16;
+            const int tp = st >> 3, kb = (st & 7) >> 1, cb = st & 1;
+            const uint8_t* p = XG + (Lc[J][cb] + 1 - tp) * RS + kb * 64 + q4 * 16;
             xh = lds16(p);
             xl = lds16(p + 256);
         };
 #pragma unroll
         for (int q = 0; q < LA; ++q) bread(q, bh[q], bl[q]);
 #pragma unroll
-        for (int st = 0; st < 16; ++st) {   // (probe) two tap groups: 96 MFMAs per tile
-            const int tp = st >> 3, kb = st & 7, cb = st % (LA + 1);
-            uint4 xh = bh[cb], xl = bl[cb];
-            if (MASKED && ((tp == 0 && !ok2) || (tp == 2 && !ok0))) {
+        for (int st = 0; st < 24; ++st) {
+            const int tp = st >> 3, kb = (st & 7) >> 1, cb = st & 1, bi = st % (LA + 1);
+            uint4 xh = bh[bi], xl = bl[bi];
+            if (MASKED && ((tp == 0 && !ok2[cb]) || (tp == 2 && !ok0[cb]))) {
                 xh = make_uint4(0, 0, 0, 0);
                 xl = xh;
             }
-            acc2[J] = mfma_f16(wd[tp][kb][0], xh, acc2[J]);
-            if (st + LA < 16) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
-#pragma unroll
-            for (int q = (3 * st) / 2; q < (3 * (st + 1)) / 2; ++q) side(q);   // (probe: all 24 steps' side work)
-            acc2[J] = mfma_f16(wd[tp][kb][1], xh, acc2[J]);
-            acc2[J] = mfma_f16(wd[tp][kb][0], xl, acc2[J]);
-            step3_schedule();
+            f32x4& c0 = acc2[J][2 * cb];
+            f32x4& c1 = acc2[J][2 * cb + 1];
+            c0 = mfma16(wd[tp][2 * kb][0], xh, c0);
+            c1 = mfma16(wd[tp][2 * kb + 1][0], xh, c1);
+            if (st + LA < 24) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
+            side(st);
+            c0 = mfma16(wd[tp][2 * kb][1], xh, c0);
+            c1 = mfma16(wd[tp][2 * kb + 1][1], xh, c1);
+            c0 = mfma16(wd[tp][2 * kb][0], xl, c0);
+            c1 = mfma16(wd[tp][2 * kb + 1][0], xl, c1);
+            step6_schedule();
         }
     };
 
-    // ---- epilogue unit (J, g) of tile et in three parts: residual read; out -> HBM; max ----
+    // ---- epilogue unit (J, sub-tile g) of tile et in three parts: residual read; out -> HBM;
+    //      max (channels chq + 16 rb .. + 3 of column 16 cb + i16) ----
     float omax = 0.f, inv2p = 0.f;
-    float* dst = nullptr;
+    float* dst[2] = {nullptr, nullptr};
     rsrc_t rs_o;            // unmasked layouts: the stores through a resource at the tile's base time
-    const uint32_t colo[2] = {(uint32_t)((toff[0] * C + chb) * 4), (uint32_t)((toff[1] * C + chb) * 4)};
-    uint32_t ocol = 0;
+    uint32_t colo[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) colo[j][cb] = (uint32_t)((toff[j][cb] * C + chq) * 4);
+    uint32_t ocol[2] = {0u, 0u};
     float4 oe, oo;
-    float sk0 = 0.f, sk1 = 0.f, sk2 = 0.f;   // SX: the lane's dot products over its 16 channels
-    size_t sxo = 0;                          // SX: spart float index of (column, wave)
-    auto epi_begin = [&](const Tile& et, int J) {
-        if (SX) sxo = (((size_t)et.b * a.T + ctime(et, 32 * J + r, toff[J])) * 4 + w) * 4;
-        else if (MASKED) dst = a.gout + ((size_t)et.b * a.T + ctime(et, 32 * J + r, toff[J])) * C + chb;
-        else { rs_o = mk_rsrc(a.gout + ((size_t)et.b * a.T + et.tb) * C); ocol = colo[J]; }
+    float sk0 = 0.f, sk1 = 0.f, sk2 = 0.f;   // SX: the lane's dot products over its 8 channels of a column
+    size_t sxo[2] = {0, 0};                  // SX: spart float index of (column, wave)
+    auto epi_begin = [&](const Tile& et_, int J) {
+        const Tile et = memt(et_);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+            const int c = 32 * J + 16 * cb + i16;
+            if (SX) sxo[cb] = (((size_t)et.b * a.T + ctime(et, c, toff[J][cb])) * 4 + w) * 4;
+            else if (MASKED) dst[cb] = a.gout + ((size_t)et.b * a.T + ctime(et, c, toff[J][cb])) * C + chq;
+            else ocol[cb] = colo[J][cb];
+        }
+        if (!SX && !MASKED) rs_o = mk_rsrc(a.gout + ((size_t)et.b * a.T + et.tb) * C);
     };
-    auto epi_part = [&](int J, int g, int part, const uint8_t* er, uint32_t mw, float inv2) {
+    auto epi_part = [&](int J, int g, int part, const uint8_t* er, const uint32_t (&mw)[2], float inv2) {
+        const int rb = g & 1, cb = g >> 1, ch = chq + 16 * rb, mg = mg0 + 2 * rb;
         if (part == 0) {
-            oe = *reinterpret_cast<const float4*>(er + Lc[J] * RS + 4 * (chb + 8 * g));
+            oe = *reinterpret_cast<const float4*>(er + Lc[J][cb] * RS + 4 * ch);
         } else if (part == 1) {
-            // (probe) the output transform's two adds per value
-            const float t0 = acc2[J][4 * g + 0] + acc2[J][4 * g + 1], t1 = acc2[J][4 * g + 1] - acc2[J][4 * g + 2];
-            const float t2 = acc2[J][4 * g + 2] + acc2[J][4 * g + 3], t3 = acc2[J][4 * g + 3] - acc2[J][4 * g + 0];
-            oo.x = fmaf(keep_if(acc2[J][4 * g + 0] + t0, mw, g), inv2, oe.x);
-            oo.y = fmaf(keep_if(acc2[J][4 * g + 1] + t1, mw, 4 + g), inv2, oe.y);
-            oo.z = fmaf(keep_if(acc2[J][4 * g + 2] + t2, mw, 8 + g), inv2, oe.z);
-            oo.w = fmaf(keep_if(acc2[J][4 * g + 3] + t3, mw, 12 + g), inv2, oe.w);
+            oo.x = fmaf(keep_if(acc2[J][g][0], mw[cb], mg), inv2, oe.x);
+            oo.y = fmaf(keep_if(acc2[J][g][1], mw[cb], 4 + mg), inv2, oe.y);
+            oo.z = fmaf(keep_if(acc2[J][g][2], mw[cb], 8 + mg), inv2, oe.z);
+            oo.w = fmaf(keep_if(acc2[J][g][3], mw[cb], 12 + mg), inv2, oe.w);
             if (SX) {
-                const float4 q0 = *reinterpret_cast<const float4*>(&W0S[chb + 8 * g]);
-                const float4 q1 = *reinterpret_cast<const float4*>(&W0S[C + chb + 8 * g]);
-                const float4 q2 = *reinterpret_cast<const float4*>(&W0S[2 * C + chb + 8 * g]);
+                const float4 q0 = *reinterpret_cast<const float4*>(&W0S[ch]);
+                const float4 q1 = *reinterpret_cast<const float4*>(&W0S[C + ch]);
+                const float4 q2 = *reinterpret_cast<const float4*>(&W0S[2 * C + ch]);
                 sk0 = fmaf(q0.w, oo.w, fmaf(q0.z, oo.z, fmaf(q0.y, oo.y, fmaf(q0.x, oo.x, sk0))));
                 sk1 = fmaf(q1.w, oo.w, fmaf(q1.z, oo.z, fmaf(q1.y, oo.y, fmaf(q1.x, oo.x, sk1))));
                 sk2 = fmaf(q2.w, oo.w, fmaf(q2.z, oo.z, fmaf(q2.y, oo.y, fmaf(q2.x, oo.x, sk2))));
-            } else if (MASKED) *reinterpret_cast<float4*>(dst + 8 * g) = oo;
-            else bst4(rs_o, ocol + 32 * g, 0u, oo);
+            } else if (MASKED) *reinterpret_cast<float4*>(dst[cb] + 16 * rb) = oo;
+            else bst4(rs_o, ocol[cb] + 64 * rb, 0u, oo);
         } else {
             omax = fmaxf(omax, fmaxf(fmaxf(fabsf(oo.x), fabsf(oo.y)), fmaxf(fabsf(oo.z), fabsf(oo.w))));
-            if (SX && g == 3) {   // the column's 16 channels done: + the other half's 16 -> spart
-                const float o0 = __shfl_xor(sk0, 32), o1 = __shfl_xor(sk1, 32), o2 = __shfl_xor(sk2, 32);
-                if (h == 0)
-                    *reinterpret_cast<float4*>(a.spart + sxo) = make_float4(sk0 + o0, sk1 + o1, sk2 + o2, 0.f);
+            if (SX && rb == 1) {   // the column's 8 channels of this lane done: + the other 3 lane quads' -> spart
+                float t0 = sk0 + __shfl_xor(sk0, 16), t1 = sk1 + __shfl_xor(sk1, 16), t2 = sk2 + __shfl_xor(sk2, 16);
+                t0 += __shfl_xor(t0, 32); t1 += __shfl_xor(t1, 32); t2 += __shfl_xor(t2, 32);
+                if (q4 == 0)
+                    *reinterpret_cast<float4*>(a.spart + sxo[cb]) = make_float4(t0, t1, t2, 0.f);
                 sk0 = sk1 = sk2 = 0.f;
             }
         }
@@ -323,7 +412,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
 #pragma unroll
         for (int k = 0; k < NU; ++k) load_unit(t0, k);
         load_masks(t0, mu_c, muh_c, me_c);
-        const uint32_t z0 = ru.zero_bits(t0, a.fn);
+        const uint32_t z0 = zbits(t0);
         gm_c = sload(a.gmax_in + t0.b);
         const float s0 = exp2i(scale_exp(gm_c));
 #pragma unroll
@@ -352,15 +441,21 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
         const float inv2 = exp2i(-(m_u + a.kd));
         if (nt.b != cu.b) gm_c = sload(a.gmax_in + nt.b);   // (usually the same clip: tile order)
         const float s_next = exp2i(scale_exp(gm_c));
-        const uint32_t zn = ru.zero_bits(nt, a.fn);
+        const uint32_t zn = zbits(nt);
         uint8_t* erc = &ER[it & 1][0];          // this tile's residual
         uint8_t* ero = &ER[(it & 1) ^ 1][0];    // the previous tile's, then the next tile's
 
         // rows 0 / 1 from the previous tile's rows 64 / 65 when it is the left neighbour (every
         // wave its channel quarter; the previous tile's g_a reads are behind the T barrier, this
         // tile's first writes to rows 64 / 65 come in B)
-        const bool cont = HALO && !FIRST && prv.b == cu.b && prv.p0 + TMS == cu.p0 && (MASKED || cu.m0 != 0);
+        // (CARRY: the previous sub-sequence's last tile left row 65 zero and the first position's
+        // g_u in row 67: rows 0 / 1 = 0 / row 67)
+        const bool cont = HALO && !FIRST && prv.b == cu.b && prv.p0 + TMS == cu.p0 && (MASKED || CARRY || cu.m0 != 0);
+        const bool fos = CARRY && cu.m0 == 0;
+        const bool cry = carry_of(cu);
+        Lv1t[1] = cry && i16 == 15 ? GROWS - 1 : Lv[1][1];   // column 63: half 1, block 1, i16 15
         const int cpo = ((lane >> 2) & 1) * 256 + 64 * w + 16 * (lane & 3);   // (side work of A)
+        const int csr = fos ? ((lane >> 3) ? GROWS - 1 : TMS) : TMS + (lane >> 3);
         uint4 cpv = make_uint4(0, 0, 0, 0);
         STAMP(11)
         // A: g_v half 0 + epilogue half 1 of the previous tile (parts 0..7)
@@ -368,9 +463,14 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
         gemm1(J0{}, [&](int kb) {
             if (!FIRST) epi_part(1, kb / 3, kb % 3, ero, me_p, inv2p);
             if (cont && lane < 16) {   // rows 64 / 65 -> 0 / 1, read one step before the write
-                if (kb == 0) cpv = lds16(XG + (TMS + (lane >> 3)) * RS + cpo);
+                if (kb == 0) {
+                    cpv = lds16(XG + csr * RS + cpo);
+                    if (fos && lane < 8) cpv = make_uint4(0, 0, 0, 0);
+                }
                 if (kb == 1) *reinterpret_cast<uint4*>(XG + (lane >> 3) * RS + cpo) = cpv;
             }
+            // a CARRY tile's row 65 is SAME padding for its own g_a (after the copy's read)
+            if (cry && lane < 8 && kb == 2) *reinterpret_cast<uint4*>(XG + (TMS + 1) * RS + cpo) = make_uint4(0, 0, 0, 0);
         });
         // B: g_v half 1 + the epilogue's parts 8..11 + g_u of half 0
         gemm1(J1{}, [&](int kb) {
@@ -384,7 +484,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
             // H: g_v of rows 0 / 1 + g_u of half 1; then g_u of rows 0 / 1
             gemm1(J2{}, [&](int kb) { gu_part(1, kb >> 1, kb & 1, f_u); });
 #pragma unroll
-            for (int q = 0; q < 8; ++q) gu_part(2, q >> 1, q & 1, f_u);
+            for (int q = 0; q < 4; ++q) gu_part(2, q >> 1, q & 1, f_u);
         } else {
 #pragma unroll
             for (int q = 0; q < 8; ++q) gu_part(1, q >> 1, q & 1, f_u);
@@ -411,9 +511,12 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
         STAMP(9)
         prv = cu;
         inv2p = inv2;
-        me_p = me_c[1];
-        me_c[0] = me_n[0]; me_c[1] = me_n[1];
-        mu_c[0] = mu_n[0]; mu_c[1] = mu_n[1];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+            me_p[cb] = me_c[1][cb];
+            me_c[0][cb] = me_n[0][cb]; me_c[1][cb] = me_n[1][cb];
+            mu_c[0][cb] = mu_n[0][cb]; mu_c[1][cb] = mu_n[1][cb];
+        }
         muh_c = muh_n;
     };
     tile_body(std::true_type{}, (int)blockIdx.x, 0);
@@ -432,24 +535,9 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_wp(BwdArgsS a, Layout ly) {
     STAMP_FLUSH(a.stamps)
 }
 
-// max |x| over each clip's n elements -> out[b] (atomic max of the float bits)
-__global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, size_t n, int chunks,
-                                                unsigned* __restrict__ out) {
-    const int b = blockIdx.x / chunks, ch = blockIdx.x - b * chunks;
-    const size_t len = n / chunks;
-    const float4* p = reinterpret_cast<const float4*>(x + (size_t)b * n + (size_t)ch * len);
-    float m = 0.f;
-    for (size_t i = threadIdx.x; i < len / 4; i += 256) {
-        const float4 v = p[i];
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    }
-    m = wave_max(m);
-    if ((threadIdx.x & 63) == 0) atomicMax(out + b, __float_as_uint(m));
-}
-
 }  // namespace
 
-bool launch_block_bwd_winoprobe(const BwdArgsS& a0, hipStream_t s) {
+void launch_block_bwd_s16(const BwdArgsS& a0, hipStream_t s) {
     BwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
     a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));
@@ -458,15 +546,18 @@ bool launch_block_bwd_winoprobe(const BwdArgsS& a0, hipStream_t s) {
     Layout ly;
     const bool masked = pick_layout(a.n, ly);
     const bool oneseg = !masked && ly.M == TMS;
-#define BWD_LAUNCH(M, O, D, X) hipLaunchKernelGGL((k_block_bwd_wp<M, O, D, X>), grid, dim3(FT), 0, s, a, ly)
-    if (masked) { if (a.dadd) BWD_LAUNCH(true, false, true, false); else BWD_LAUNCH(true, false, false, false); }
-    else if (oneseg) {
-        if (a.dadd) BWD_LAUNCH(false, true, true, false);
-        else if (a.spart) BWD_LAUNCH(false, true, false, true);
-        else BWD_LAUNCH(false, true, false, false);
-    } else { if (a.dadd) BWD_LAUNCH(false, false, true, false); else BWD_LAUNCH(false, false, false, false); }
+    if (a.spart && (!oneseg || a.dadd || a.d != 1)) { fprintf(stderr, "block_bwd_s: spart needs d = 1, no D\n"); abort(); }
+    const bool whole = oneseg && a.n == TMS;
+#define BWD_LAUNCH(M, O, D, X, W) hipLaunchKernelGGL((k_block_bwd_s16<M, O, D, X, W>), grid, dim3(FT), 0, s, a, ly)
+    if (masked) { if (a.dadd) BWD_LAUNCH(true, false, true, false, false); else BWD_LAUNCH(true, false, false, false, false); }
+    else if (whole && !a.spart) {
+        if (a.dadd) BWD_LAUNCH(false, true, true, false, true); else BWD_LAUNCH(false, true, false, false, true);
+    } else if (oneseg) {
+        if (a.dadd) BWD_LAUNCH(false, true, true, false, false);
+        else if (a.spart) BWD_LAUNCH(false, true, false, true, false);
+        else BWD_LAUNCH(false, true, false, false, false);
+    } else { if (a.dadd) BWD_LAUNCH(false, false, true, false, false); else BWD_LAUNCH(false, false, false, false, false); }
 #undef BWD_LAUNCH
-    return true;
 }
 
 }  // namespace ast

@@ -26,7 +26,7 @@
 // floor of 6.2k; moving the loads / conversions between phases does not change the tile time.
 // non-temporal (gfx950 CPol nt) row loads and e_{l+1} stores: every row streams through once, and
 // the stores are whole 128-B lines (round 6: -1.0 % per launch from the stores, -0.4 % from the
-// loads, profiles/r6_diag/nt_ab.txt); -DSW_FWD_DEFAULT_POLICY (A/B builds) restores the default
+// loads, profiles/r6_diag/block_ab.txt); -DSW_FWD_DEFAULT_POLICY (A/B builds) restores the default
 #ifndef SW_FWD_DEFAULT_POLICY
 #define SW_LD_AUX 2
 #define SW_ST_AUX 2
@@ -49,7 +49,11 @@ constexpr int LA = 2;                 // B-fragment lookahead (steps)
 // (e0_val: three samples per row, W0 / b0 of the lane's four channels in registers) instead of
 // loaded, so the start conv writes no e_0 tensor (model.py:82-93 folded into block 0)
 template <bool MASKED, bool ONESEG, bool XIN>
-__global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
+__global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout) {
+    // the layout as compile-time constants (pick_layout: one segment or masked: M = 64 with two
+    // halo rows; else segments of SEGM = 32 with their pad rows), not the launch argument
+    constexpr bool GEO1 = ONESEG || MASKED;
+    const Layout ly = {GEO1 ? TMS : SEGM, GEO1 ? TMS + 2 : (TMS / SEGM) * (SEGM + 2)};
     __shared__ __attribute__((aligned(16))) uint8_t IMG[ISLOT];     // split relu(e_l) image
     __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];   // fp32 e_l (residual) rows
     __shared__ __attribute__((aligned(16))) uint8_t XV[TMS * RS];   // split v image
@@ -475,22 +479,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s(FwdArgsS a, Layout ly) {
 
 }  // namespace
 
-#ifdef ASTYLE_FWD_VARIANTS
-// tools/variants/ build only (libastyle_fwdvariants.so): the measured-slower alternatives of this
-// kernel, bit-identical, selected by ASTYLE_FWD_ROLES=1 / ASTYLE_FWD_DB=1
-bool launch_block_fwd_roles(const FwdArgsS& a, hipStream_t s);   // tools/variants/block_fwd_roles.hip
-bool launch_block_fwd_db(const FwdArgsS& a, hipStream_t s);      // tools/variants/block_fwd_db.hip
-bool launch_block_fwd_winoprobe(const FwdArgsS& a, hipStream_t s);   // tools/variants/block_fwd_winoprobe.hip
-static bool env_on(const char* k) { const char* e = getenv(k); return e && atoi(e) != 0; }
-#endif
-
 void launch_block_fwd_s(const FwdArgsS& a0, hipStream_t s) {
-#ifdef ASTYLE_FWD_VARIANTS
-    // (block 0 recomputes e_0 from x, which the variants do not: they run blocks 1..)
-    if (!a0.xin && env_on("ASTYLE_FWD_ROLES")) { launch_block_fwd_roles(a0, s); return; }
-    if (!a0.xin && env_on("ASTYLE_FWD_DB")) { launch_block_fwd_db(a0, s); return; }
-    if (env_on("ASTYLE_FWD_WINOPROBE")) { launch_block_fwd_winoprobe(a0, s); return; }
-#endif
     FwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
     a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));

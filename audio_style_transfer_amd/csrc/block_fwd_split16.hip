@@ -1,18 +1,15 @@
-// TIMING PROBE (tools-only variant, results WRONG by design): the cost structure a Winograd
-// F(2,3) GEMM 1 would have inside this kernel's register and LDS budget -- GEMM 1 runs two of the
-// three tap groups (96 instead of 144 MFMAs per tile, as Winograd's four transformed products
-// over 32 output pairs), the conversion splits every unit a second time into the image row's
-// pad bytes (Winograd converts ~2x the rows: 128 transformed rows for 66 plain ones, each an
-// add + a split), and epilogue 1 adds the output transform's two adds per value.  The real
-// Winograd kernel would also need ~30 KB more LDS and ~10 more registers than this kernel has
-// (DESIGN.md §3), so this measures an upper bound of its gain.  ASTYLE_FWD_WINOPROBE=1 in the
-// libastyle_fwdvariants.so build.
+// ASTYLE_MFMA16=1 (round 6): the forward block kernel of block_fwd_split.hip on
+// v_mfma_f32_16x16x32_f16 fragments (splitwave.h "16x16x32"; the weights are packed for it when the
+// knob is set).  Same structure, phases and numerics class; the K accumulation order differs, so
+// results match the default kernels to fp32 rounding, not bit for bit.  Measured (DESIGN.md §3,
+// round 6): 4-5 % slower per launch than the 32x32x16 default at equal data; kept as the
+// measured alternative, not the default.
 //
 // Split-fp16 encoder block forward (precision 2): model.py:95-116 for one block,
 //   u = dconv_d(relu(e_l)) + b_d        (masked.py:110-160, K = 3, SAME zero padding)
 //   e_{l+1} = e_l + W_r^T relu(u) + b_r
-// fp32 storage, v_mfma_f32_32x32x16_f16 on split fp16 operands, fp32 accumulation and fp32
-// epilogues (splitwave.h).
+// fp32 storage, v_mfma_f32_16x16x32_f16 on split fp16 operands (round 6; 32x32x16 before), fp32
+// accumulation and fp32 epilogues (splitwave.h).
 //
 // One workgroup per CU (wave w owns output channels 32 w .. 32 w + 31), persistent over tiles
 // of 64 positions, one wave per SIMD: every epilogue runs in the shadow of MFMAs.  The two
@@ -34,6 +31,13 @@
 //   D  GEMM 2, half 1; carries the conversion of tile i+1 (image + residual)
 // Round-2 measurements of this structure: ~13k cycles per tile against an MFMA
 // floor of 6.2k; moving the loads / conversions between phases does not change the tile time.
+// non-temporal (gfx950 CPol nt) row loads and e_{l+1} stores: every row streams through once, and
+// the stores are whole 128-B lines (round 6: -1.0 % per launch from the stores, -0.4 % from the
+// loads, profiles/r6_diag/block_ab.txt); -DSW_FWD_DEFAULT_POLICY (A/B builds) restores the default
+#ifndef SW_FWD_DEFAULT_POLICY
+#define SW_LD_AUX 2
+#define SW_ST_AUX 2
+#endif
 #include "splitwave.h"
 #include <algorithm>
 #include <cstdio>
@@ -52,7 +56,11 @@ constexpr int LA = 2;                 // B-fragment lookahead (steps)
 // (e0_val: three samples per row, W0 / b0 of the lane's four channels in registers) instead of
 // loaded, so the start conv writes no e_0 tensor (model.py:82-93 folded into block 0)
 template <bool MASKED, bool ONESEG, bool XIN>
-__global__ void __launch_bounds__(FT, 1) k_block_fwd_wp(FwdArgsS a, Layout ly) {
+__global__ void __launch_bounds__(FT, 1) k_block_fwd_s16(FwdArgsS a, Layout) {
+    // the layout as compile-time constants (pick_layout: one segment or masked: M = 64 with two
+    // halo rows; else segments of SEGM = 32 with their pad rows), not the launch argument
+    constexpr bool GEO1 = ONESEG || MASKED;
+    const Layout ly = {GEO1 ? TMS : SEGM, GEO1 ? TMS + 2 : (TMS / SEGM) * (SEGM + 2)};
     __shared__ __attribute__((aligned(16))) uint8_t IMG[ISLOT];     // split relu(e_l) image
     __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];   // fp32 e_l (residual) rows
     __shared__ __attribute__((aligned(16))) uint8_t XV[TMS * RS];   // split v image
@@ -66,7 +74,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_wp(FwdArgsS a, Layout ly) {
     const int ntiles = a.B * tiles;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int r = lane & 31, h = lane >> 5;
+    const int i16 = lane & 15, q4 = lane >> 4;   // 16x16x32 fragment lane (splitwave.h)
     const int G = (int)gridDim.x;
     STAMP_DECL
 
@@ -92,13 +100,17 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_wp(FwdArgsS a, Layout ly) {
     pin_all(wd, wr);
     if (tid < C) { BIAS[tid] = a.bd[tid]; BIAS[C + tid] = a.br[tid]; }
 
-    int Lc[2], toff[2];
+    // image row and time offset of the lane's column 16 cb + i16 of column half j
+    int Lc[2][2], toff[2][2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        Lc[j] = frow(32 * j + r, ly);
-        toff[j] = MASKED ? 0 : row_toff(Lc[j], ly, a.d);
-    }
-    const int chb = 32 * w + 4 * h;   // first channel of this lane's accumulator group g = 0
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+            Lc[j][cb] = frow(32 * j + 16 * cb + i16, ly);
+            toff[j][cb] = MASKED ? 0 : row_toff(Lc[j][cb], ly, a.d);
+        }
+    const int chq = 32 * w + 4 * q4;  // first channel of this lane's sub-tiles (+ 16 rb)
+    const int mg0 = q4 >> 1;          // mask group of row block 0 (mgrp: + 2 rb); word h = q4 & 1
     auto ctime = [&](const Tile& t, int cc, int to) { return col_time<MASKED>(t, cc, to, a.fn, a.d); };
 
     // ---- row units: unit k, lane -> image row L = 8 k + lr, channels cq .. cq + 3 ----
@@ -186,13 +198,6 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_wp(FwdArgsS a, Layout ly) {
         uint8_t* p = IMG + imgo + 8 * k * RS;
         *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
         *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
-        {   // (probe) a transformed row's add + split, stored in the row's pad bytes
-            uint32_t g01, m01, g23, m23;
-            split2s((v.x + v.y) * sk, (v.y - v.x) * sk, g01, m01);
-            split2s((v.z + v.w) * sk, (v.w - v.z) * sk, g23, m23);
-            uint8_t* q = IMG + (lr + 8 * k) * RS + 512;
-            *reinterpret_cast<uint2*>(q) = make_uint2(g01 ^ m01, g23 ^ m23);
-        }
     };
 
     // e_{l+1} > 0 words of a finished tile -> next layer's positions (wave w: columns 16 w..)
@@ -211,30 +216,32 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_wp(FwdArgsS a, Layout ly) {
     //      its quarter), and leaves for HBM from there as whole 128-B lines (flush: 8 columns x
     //      the wave's 32 channels per store); stored straight from the accumulator layout, each
     //      store would touch 32 lines 32 B at a time ----
-    f32x16 acc2[2];                    // y of the pending epilogue 2
+    f32x4 acc2[2][4];                  // y of the pending epilogue 2 (sub-tiles n = 2 cb + rb)
     Tile prv = tile_of(blockIdx.x);
     float inv2p = 0.f;
     float emax = 0.f;
-    uint32_t mb[2] = {0u, 0u};
+    uint32_t mb[2][2] = {{0u, 0u}, {0u, 0u}};
     float4 e2e, e2b, e2o;
     auto epi2_begin = [&]() {   // (emax runs on over the workgroup's consecutive tiles of one clip)
-        mb[0] = mb[1] = 0u;
+        mb[0][0] = mb[0][1] = mb[1][0] = mb[1][1] = 0u;
     };
+    // unit u = (j, sub-tile g): channels chq + 16 rb .. + 3 of column 16 cb + i16
     auto epi2_part = [&](int u, int part, uint8_t* erp) {
-        const int j = u >> 2, g = u & 3;
+        const int j = u >> 2, g = u & 3, rb = g & 1, cb = g >> 1;
+        const int ch = chq + 16 * rb;
         if (part == 0) {
-            e2e = *reinterpret_cast<const float4*>(erp + Lc[j] * RS + 4 * (chb + 8 * g));
-            e2b = *reinterpret_cast<const float4*>(&BIAS[C + chb + 8 * g]);
+            e2e = *reinterpret_cast<const float4*>(erp + Lc[j][cb] * RS + 4 * ch);
+            e2b = *reinterpret_cast<const float4*>(&BIAS[C + ch]);
         } else if (part == 1) {
-            e2o.x = e2e.x + fmaf(acc2[j][4 * g + 0], inv2p, e2b.x);
-            e2o.y = e2e.y + fmaf(acc2[j][4 * g + 1], inv2p, e2b.y);
-            e2o.z = e2e.z + fmaf(acc2[j][4 * g + 2], inv2p, e2b.z);
-            e2o.w = e2e.w + fmaf(acc2[j][4 * g + 3], inv2p, e2b.w);
-            *reinterpret_cast<float4*>(erp + Lc[j] * RS + 4 * (chb + 8 * g)) = e2o;
+            e2o.x = e2e.x + fmaf(acc2[j][g][0], inv2p, e2b.x);
+            e2o.y = e2e.y + fmaf(acc2[j][g][1], inv2p, e2b.y);
+            e2o.z = e2e.z + fmaf(acc2[j][g][2], inv2p, e2b.z);
+            e2o.w = e2e.w + fmaf(acc2[j][g][3], inv2p, e2b.w);
+            *reinterpret_cast<float4*>(erp + Lc[j][cb] * RS + 4 * ch) = e2o;
         } else {
             emax = fmaxf(emax, fmaxf(fmaxf(fabsf(e2o.x), fabsf(e2o.y)), fmaxf(fabsf(e2o.z), fabsf(e2o.w))));
-            // bit mbit(4 g + q) = 4 q + g of the column's word (common.h)
-            mb[j] = or_pos_bits4(mb[j], e2o.x, e2o.y, e2o.z, e2o.w, g);
+            // bit mbit(4 g' + k) = 4 k + g' of the column's word h = q4 & 1 (common.h, splitwave.h mgrp)
+            mb[j][cb] = or_pos_bits4(mb[j][cb], e2o.x, e2o.y, e2o.z, e2o.w, mg0 + 2 * rb);
         }
     };
     // flush piece (j, q): columns 32 j + 8 q + lr (lr = lane >> 3), channels cq .. cq + 3; part 0
@@ -254,14 +261,18 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_wp(FwdArgsS a, Layout ly) {
             bst4(mk_rsrc(a.eout + ((size_t)prv.b * a.T + prv.tb) * C), fl_lane, (uint32_t)(tu * C * 4), fl4);
         }
     };
-    // words and column times to LDS (all lanes write: identical values per column)
+    // words and column times to LDS: a column's word h holds the groups of lane quads h and h + 2
+    // (the lanes 32 apart); the quads 0 / 1 write it, all four the column's time (identical values)
     auto epi2_words = [&]() {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int c = 32 * j + r;
-            MBE[c * 8 + 4 * h + w] = (uint16_t)mb[j];
-            MBT[c] = ctime(prv, c, toff[j]);
-        }
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+                const int c = 32 * j + 16 * cb + i16;
+                const uint32_t wv = mb[j][cb] | (uint32_t)__shfl_xor((int)mb[j][cb], 32);
+                if (q4 < 2) MBE[c * 8 + 4 * q4 + w] = (uint16_t)wv;
+                MBT[c] = ctime(prv, c, toff[j][cb]);
+            }
     };
     // max |e_{l+1}| of clip prv.b -> gmax_out, once per run of tiles of one clip (with the
     // clip-interleaved tile order a workgroup usually keeps its clip for the whole launch)
@@ -275,38 +286,41 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_wp(FwdArgsS a, Layout ly) {
     // v = relu(u) 2^m_v = relu(acc 2^(m_v - m_e - k_d) + b_d 2^m_v): the scale folded into the fma
     // (powers of two: the same values); the u > 0 bits from the split's rtz hi halves (splitwave.h
     // nz2; SW_UBITS_EXACT: from v itself)
-    f32x16 acc1[2];
+    f32x4 acc1[2][4];
     float a1 = 0.f;
     float bs_sv = -1.f;   // the v scale BDS holds
     uint32_t mu_w = 0;
     float4 e1v;
+    // sub-tile g of column half j (rb = g & 1, cb = g >> 1); after both row blocks of a column
+    // block the column's u > 0 word (the other two groups from the lane quad q4 ^ 2)
     auto epi1_part = [&](int j, int g, int part) {
+        const int rb = g & 1, cb = g >> 1, ch = chq + 16 * rb;
         if (part == 0) {
-            const float4 b4 = *reinterpret_cast<const float4*>(&BDS[chb + 8 * g]);
-            // (probe) the output transform's two adds per value
-            const float t0 = acc1[j][4 * g + 0] + acc1[j][4 * g + 1], t1 = acc1[j][4 * g + 1] - acc1[j][4 * g + 2];
-            const float t2 = acc1[j][4 * g + 2] + acc1[j][4 * g + 3], t3 = acc1[j][4 * g + 3] - acc1[j][4 * g + 0];
-            e1v.x = fmaxf(fmaf(acc1[j][4 * g + 0] + t0, a1, b4.x), 0.f);
-            e1v.y = fmaxf(fmaf(acc1[j][4 * g + 1] + t1, a1, b4.y), 0.f);
-            e1v.z = fmaxf(fmaf(acc1[j][4 * g + 2] + t2, a1, b4.z), 0.f);
-            e1v.w = fmaxf(fmaf(acc1[j][4 * g + 3] + t3, a1, b4.w), 0.f);
+            const float4 b4 = *reinterpret_cast<const float4*>(&BDS[ch]);
+            e1v.x = fmaxf(fmaf(acc1[j][g][0], a1, b4.x), 0.f);
+            e1v.y = fmaxf(fmaf(acc1[j][g][1], a1, b4.y), 0.f);
+            e1v.z = fmaxf(fmaf(acc1[j][g][2], a1, b4.z), 0.f);
+            e1v.w = fmaxf(fmaf(acc1[j][g][3], a1, b4.w), 0.f);
         } else {
             uint32_t h01, l01, h23, l23;
             split2(e1v.x, e1v.y, h01, l01);
             split2(e1v.z, e1v.w, h23, l23);
-            uint8_t* p = XV + (32 * j + r) * RS + 2 * (chb + 8 * g);
+            const int c = 32 * j + 16 * cb + i16;
+            uint8_t* p = XV + c * RS + 2 * ch;
             *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
             *reinterpret_cast<uint2*>(p + 256) = make_uint2(l01, l23);
 #ifdef SW_UBITS_EXACT
-            mu_w = or_pos_bits4(mu_w, e1v.x, e1v.y, e1v.z, e1v.w, g);
-            if (g == 3) {
-                MBU[(32 * j + r) * 8 + 4 * h + w] = (uint16_t)mu_w;
+            mu_w = or_pos_bits4(mu_w, e1v.x, e1v.y, e1v.z, e1v.w, mg0 + 2 * rb);
+            if (rb == 1) {
+                const uint32_t wv = mu_w | (uint32_t)__shfl_xor((int)mu_w, 32);
+                if (q4 < 2) MBU[c * 8 + 4 * q4 + w] = (uint16_t)wv;
                 mu_w = 0;
             }
 #else
-            mu_w = or_bits4(mu_w, h01, h23, g);
-            if (g == 3) {
-                MBU[(32 * j + r) * 8 + 4 * h + w] = (uint16_t)mask16(mu_w);
+            mu_w = or_bits4(mu_w, h01, h23, mg0 + 2 * rb);
+            if (rb == 1) {
+                const uint32_t wv = mask16(mu_w | (uint32_t)__shfl_xor((int)mu_w, 32));
+                if (q4 < 2) MBU[c * 8 + 4 * q4 + w] = (uint16_t)wv;
                 mu_w = 0;
             }
 #endif
@@ -314,67 +328,85 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_wp(FwdArgsS a, Layout ly) {
     };
 
 
-    // ---- GEMM 1 of column half J over the image; side work per step ----
+    // ---- GEMM 1 of column half J over the image; side work per step.  Step st = (tap, K block
+    //      kb of 32, column block cb): 3 split products x 2 row blocks (splitwave.h) ----
     auto gemm1h = [&](auto j_tag, auto side, const Tile& cu) {
         constexpr int J = decltype(j_tag)::value;
-        bool ok0 = true, ok2 = true;
+        bool ok0[2] = {true, true}, ok2[2] = {true, true};
         if (MASKED) {
-            const int pc = cu.p0 + 32 * J + r;
-            const int m = pc - (int)fdiv((uint32_t)pc, a.fn) * a.n;
-            ok0 = m > 0;
-            ok2 = m < a.n - 1;
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+                const int pc = cu.p0 + 32 * J + 16 * cb + i16;
+                const int m = pc - (int)fdiv((uint32_t)pc, a.fn) * a.n;
+                ok0[cb] = m > 0;
+                ok2[cb] = m < a.n - 1;
+            }
         }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc1[J][i] = 0.f;
-        // B fragments are read LA steps ahead (a step is only 3 MFMAs: one step ahead leaves
-        // the LDS latency exposed)
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc1[J][n][i] = 0.f;
+        // B fragments are read LA steps ahead (one step ahead leaves the LDS latency exposed)
         uint4 bh[LA + 1], bl[LA + 1];
         auto bread = [&](int st, uint4& xh, uint4& xl) {
-            const int tp = st >> 3, kb = st & 7;
-            const uint8_t* p = IMG + (Lc[J] + tp - 1) * RS + kb * 32 + h * 16;
+            const int tp = st >> 3, kb = (st & 7) >> 1, cb = st & 1;
+            const uint8_t* p = IMG + (Lc[J][cb] + tp - 1) * RS + kb * 64 + q4 * 16;
             xh = lds16(p);
             xl = lds16(p + 256);
         };
 #pragma unroll
         for (int q = 0; q < LA; ++q) bread(q, bh[q], bl[q]);
 #pragma unroll
-        for (int st = 0; st < 16; ++st) {   // (probe) two tap groups: 96 MFMAs per tile
-            const int tp = st >> 3, kb = st & 7, cb = st % (LA + 1);
-            uint4 xh = bh[cb], xl = bl[cb];
-            if (MASKED && ((tp == 0 && !ok0) || (tp == 2 && !ok2))) {
+        for (int st = 0; st < 24; ++st) {
+            const int tp = st >> 3, kb = (st & 7) >> 1, cb = st & 1, bi = st % (LA + 1);
+            uint4 xh = bh[bi], xl = bl[bi];
+            if (MASKED && ((tp == 0 && !ok0[cb]) || (tp == 2 && !ok2[cb]))) {
                 xh = make_uint4(0, 0, 0, 0);
                 xl = xh;
             }
-            acc1[J] = mfma_f16(wd[tp][kb][0], xh, acc1[J]);
-            if (st + LA < 16) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
+            f32x4& c0 = acc1[J][2 * cb];
+            f32x4& c1 = acc1[J][2 * cb + 1];
+            c0 = mfma16(wd[tp][2 * kb][0], xh, c0);
+            c1 = mfma16(wd[tp][2 * kb + 1][0], xh, c1);
+            if (st + LA < 24) bread(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
             side(st);
-            acc1[J] = mfma_f16(wd[tp][kb][1], xh, acc1[J]);
-            acc1[J] = mfma_f16(wd[tp][kb][0], xl, acc1[J]);
-            step3_schedule();
+            c0 = mfma16(wd[tp][2 * kb][1], xh, c0);
+            c1 = mfma16(wd[tp][2 * kb + 1][1], xh, c1);
+            c0 = mfma16(wd[tp][2 * kb][0], xl, c0);
+            c1 = mfma16(wd[tp][2 * kb + 1][0], xl, c1);
+            step6_schedule();
         }
     };
-    // ---- GEMM 2 of column half J over the v image ----
+    // ---- GEMM 2 of column half J over the v image; step st = (K block st >> 1, column block
+    //      st & 1) ----
     auto gemm2h = [&](auto j_tag, auto side) {
         constexpr int J = decltype(j_tag)::value;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc2[J][i] = 0.f;
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc2[J][n][i] = 0.f;
         uint4 bh[LA + 1], bl[LA + 1];
-        auto bload = [&](int kb, uint4& xh, uint4& xl) {
-            const uint8_t* p = XV + (32 * J + r) * RS + kb * 32 + h * 16;
+        auto bload = [&](int st, uint4& xh, uint4& xl) {
+            const uint8_t* p = XV + (32 * J + 16 * (st & 1) + i16) * RS + (st >> 1) * 64 + q4 * 16;
             xh = lds16(p);
             xl = lds16(p + 256);
         };
 #pragma unroll
         for (int q = 0; q < LA; ++q) bload(q, bh[q], bl[q]);
 #pragma unroll
-        for (int kb = 0; kb < 8; ++kb) {
-            const int cb = kb % (LA + 1);
-            acc2[J] = mfma_f16(wr[kb][0], bh[cb], acc2[J]);
-            if (kb + LA < 8) bload(kb + LA, bh[(kb + LA) % (LA + 1)], bl[(kb + LA) % (LA + 1)]);
-            side(kb);
-            acc2[J] = mfma_f16(wr[kb][1], bh[cb], acc2[J]);
-            acc2[J] = mfma_f16(wr[kb][0], bl[cb], acc2[J]);
-            step3_schedule();
+        for (int st = 0; st < 8; ++st) {
+            const int kb = st >> 1, cb = st & 1, bi = st % (LA + 1);
+            f32x4& c0 = acc2[J][2 * cb];
+            f32x4& c1 = acc2[J][2 * cb + 1];
+            c0 = mfma16(wr[2 * kb][0], bh[bi], c0);
+            c1 = mfma16(wr[2 * kb + 1][0], bh[bi], c1);
+            if (st + LA < 8) bload(st + LA, bh[(st + LA) % (LA + 1)], bl[(st + LA) % (LA + 1)]);
+            side(st);
+            c0 = mfma16(wr[2 * kb][1], bh[bi], c0);
+            c1 = mfma16(wr[2 * kb + 1][1], bh[bi], c1);
+            c0 = mfma16(wr[2 * kb][0], bl[bi], c0);
+            c1 = mfma16(wr[2 * kb + 1][0], bl[bi], c1);
+            step6_schedule();
         }
     };
     using J0 = std::integral_constant<int, 0>;
@@ -424,32 +456,22 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_wp(FwdArgsS a, Layout ly) {
         // A: GEMM 1 half 0 + epilogue 2 of the previous tile
         if (!FIRST) {
             epi2_begin();
-            gemm1h(J0{}, [&](int st) {   // (probe: 16 steps carry the 24-step side work)
-#pragma unroll
-                for (int q = (3 * st) / 2; q < (3 * (st + 1)) / 2; ++q) {
-                    epi2_part(q / 3, q % 3, erp);
-                    if (q >= 12 && q < 20) flush_part(0, (q - 12) >> 1, q & 1, erp);
-                    if (q % 3 == 1 && q < 15) load_unit(nt, q / 3);
-                }
+            gemm1h(J0{}, [&](int st) {
+                epi2_part(st / 3, st % 3, erp);
+                if (st >= 12 && st < 20) flush_part(0, (st - 12) >> 1, st & 1, erp);
+                if (st % 3 == 1 && st < 15) load_unit(nt, st / 3);   // rows of tile i+1: units 0..4
             }, cu);
             epi2_words();
             if (cu.b != prv.b) epi2_max();
         } else {
-            gemm1h(J0{}, [&](int st) {
-#pragma unroll
-                for (int q = (3 * st) / 2; q < (3 * (st + 1)) / 2; ++q)
-                    if (q % 3 == 1 && q < 15) load_unit(nt, q / 3);
-            }, cu);
+            gemm1h(J0{}, [&](int st) { if (st % 3 == 1 && st < 15) load_unit(nt, st / 3); }, cu);
         }
         STAMP(5)
         // B: GEMM 1 half 1 + epilogue 1 of half 0
         gemm1h(J1{}, [&](int st) {
-#pragma unroll
-            for (int q = (3 * st) / 2; q < (3 * (st + 1)) / 2; ++q) {
-                if (q < 8) epi1_part(0, q >> 1, q & 1);
-                else if (!FIRST && q < 16) flush_part(1, (q - 8) >> 1, q & 1, erp);
-                if (q >= 11 && q % 3 == 2) load_unit(nt, 5 + (q - 11) / 3);
-            }
+            if (st < 8) epi1_part(0, st >> 1, st & 1);
+            else if (!FIRST && st < 16) flush_part(1, (st - 8) >> 1, st & 1, erp);
+            if (st >= 11 && st % 3 == 2) load_unit(nt, 5 + (st - 11) / 3);   // units 5..8: 11 14 17 20
         }, cu);
         lds_barrier();   // v image half 0, u > 0 words half 0, e > 0 words of tile i-1
         STAMP(1)
@@ -498,7 +520,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_wp(FwdArgsS a, Layout ly) {
 
 }  // namespace
 
-bool launch_block_fwd_winoprobe(const FwdArgsS& a0, hipStream_t s) {
+void launch_block_fwd_s16(const FwdArgsS& a0, hipStream_t s) {
     FwdArgsS a = a0;
     a.fn = make_fdiv((uint32_t)a.n);
     a.ft = make_fdiv((uint32_t)(SW_TILE_INTERLEAVE ? a.B : a.T / TMS));
@@ -506,11 +528,11 @@ bool launch_block_fwd_winoprobe(const FwdArgsS& a0, hipStream_t s) {
     const dim3 grid(std::min(nt, a.cus > 0 ? std::min(a.cus, sw::num_cus()) : sw::num_cus()));
     Layout ly;
     const bool masked = pick_layout(a.n, ly);
-    if (masked) hipLaunchKernelGGL((k_block_fwd_wp<true, false, false>), grid, dim3(FT), 0, s, a, ly);
-    else if (ly.M == TMS && a.xin) hipLaunchKernelGGL((k_block_fwd_wp<false, true, true>), grid, dim3(FT), 0, s, a, ly);
-    else if (ly.M == TMS) hipLaunchKernelGGL((k_block_fwd_wp<false, true, false>), grid, dim3(FT), 0, s, a, ly);
-    else hipLaunchKernelGGL((k_block_fwd_wp<false, false, false>), grid, dim3(FT), 0, s, a, ly);
-    return true;
+    if (a.xin && (masked || ly.M != TMS || a.d != 1)) { fprintf(stderr, "block_fwd_s: xin needs d = 1\n"); abort(); }
+    if (masked) hipLaunchKernelGGL((k_block_fwd_s16<true, false, false>), grid, dim3(FT), 0, s, a, ly);
+    else if (ly.M == TMS && a.xin) hipLaunchKernelGGL((k_block_fwd_s16<false, true, true>), grid, dim3(FT), 0, s, a, ly);
+    else if (ly.M == TMS) hipLaunchKernelGGL((k_block_fwd_s16<false, true, false>), grid, dim3(FT), 0, s, a, ly);
+    else hipLaunchKernelGGL((k_block_fwd_s16<false, false, false>), grid, dim3(FT), 0, s, a, ly);
 }
 
 }  // namespace ast

@@ -167,6 +167,10 @@ struct BwdArgsC {
 //   wrf [4 w][8 kb][2 hl][64]:                                     W_r[16 kb + 8 h + e][32 w + m]
 //   wrb [4 w][8 kb][2 hl][64]:                                     W_r[32 w + m][16 kb + 8 h + e]
 //   wdb [4 w][3 tap][8 kb][2 hl][64]:                              W_d[tap][32 w + m][16 kb + 8 h + e]
+// ASTYLE_MFMA16=1 (the 16x16x32 kernels, block_*_split16.hip): the same arrays hold 16x16x32 A
+// fragments, slot s = 2 kb + rb (K block kb of 32, row block rb), lane (i, q) = (lane & 15, lane >> 4):
+//   wdf: W_d[tap][32 kb + 8 q + e][32 w + 16 rb + i]     wrf: W_r[32 kb + 8 q + e][32 w + 16 rb + i]
+//   wrb: W_r[32 w + 16 rb + i][32 kb + 8 q + e]          wdb: W_d[tap][32 w + 16 rb + i][32 kb + 8 q + e]
 // gmax_*: per clip max |x| of a tensor as float bits (atomic max of the non-negative bit pattern).
 // Division by a launch-invariant divisor without the signed-division expansion (~17 scalar
 // instructions each): q = mulhi(x, m) >> s with m = ceil(2^(31 + l) / n), 2^l >= n, exact for
@@ -325,7 +329,9 @@ void launch_block_bwd(const BwdArgs& a, hipStream_t s);
 void launch_block_fwd_c(const FwdArgsC& a, hipStream_t s);
 void launch_block_bwd_c(const BwdArgsC& a, hipStream_t s);
 void launch_block_fwd_s(const FwdArgsS& a, hipStream_t s);
+void launch_block_fwd_s16(const FwdArgsS& a, hipStream_t s);   // ASTYLE_MFMA16=1
 void launch_block_bwd_s(const BwdArgsS& a, hipStream_t s);
+void launch_block_bwd_s16(const BwdArgsS& a, hipStream_t s);   // ASTYLE_MFMA16=1
 void launch_absmax(const float* x, size_t per_clip, int B, unsigned* out, hipStream_t s);
 template <typename S>
 void launch_bottleneck_fwd(const S* e, float* y, const float* wb, const float* bb,

@@ -45,9 +45,13 @@ struct Layout {            // uniform per launch (pick_layout)
 // One segment with halo rows when a tile lies inside one sub-sequence (n % 64 == 0); whole
 // sub-sequences of 32 positions with their own zero pad rows (n == 32); otherwise per-column
 // tap masks over 64 gathered positions (MASKED, n < 32).
+// The segment layout is always n = SEGM = 32 (n < 64 dividing 64, n >= 32): the device helpers
+// below divide by the constants SEGM / SEGM + 2, not by ly.M (a runtime division is ~20 VALU, and
+// under register pressure the compiler recomputes these per tile, round 6)
+constexpr int SEGM = 32;
 inline bool pick_layout(int n, Layout& ly) {
     if (n % TMS == 0) { ly.M = TMS; ly.nrows = TMS + 2; return false; }
-    if (n < TMS && TMS % n == 0 && n >= 32) { ly.M = n; ly.nrows = (TMS / n) * (n + 2); return false; }
+    if (n == SEGM) { ly.M = n; ly.nrows = (TMS / n) * (n + 2); return false; }
     ly.M = TMS; ly.nrows = TMS + 2;
     return true;
 }
@@ -55,7 +59,7 @@ inline bool pick_layout(int n, Layout& ly) {
 int num_cus();
 
 __device__ __forceinline__ int frow(int c, const Layout& ly) {   // image row of tile column c
-    return (c / ly.M) * (ly.M + 2) + 1 + (c % ly.M);
+    return ly.M == TMS ? c + 1 : (c / SEGM) * (SEGM + 2) + 1 + (c % SEGM);
 }
 
 // time offset of image row L from the tile's base time (unmasked layouts):
@@ -63,7 +67,7 @@ __device__ __forceinline__ int frow(int c, const Layout& ly) {   // image row of
 //   segments of M = n: row (s, k) is position k-1 of sub-sequence j0 + s, t = tb + (k-1) d + s
 __device__ __forceinline__ int row_toff(int L, const Layout& ly, int d) {
     if (ly.M == TMS) return (L - 1) * d;
-    const int s = L / (ly.M + 2), k = L - s * (ly.M + 2);
+    const int s = L / (SEGM + 2), k = L - s * (SEGM + 2);
     return (k - 1) * d + s;
 }
 
@@ -138,8 +142,8 @@ __device__ __forceinline__ uint4 lds16(const uint8_t* p) { return *reinterpret_c
 // Their DMA reads a row of the same tile instead, so every DMA address is in bounds.
 __device__ __forceinline__ bool pad_row(int L, const Layout& ly) {
     if (ly.M == TMS) return false;
-    const int k = L % (ly.M + 2);
-    return k == 0 || k == ly.M + 1;
+    const int k = L % (SEGM + 2);
+    return k == 0 || k == SEGM + 1;
 }
 // ---- register-fed row units (block kernels): unit k (k < NU), lane -> image row
 //      L = 8 k + (lane >> 3), channels cq .. cq + 3 of the wave's quarter (32 w .. 32 w + 31):
@@ -253,6 +257,34 @@ __device__ __forceinline__ void split4(float a0, float a1, float a2, float a3, u
 __device__ __forceinline__ f32x16 mfma_f16(uint4 a, uint4 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
                                                    __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+// ---- the 16x16x32 form (ASTYLE_MFMA16=1: block_fwd_split16.hip, block_bwd_split16.hip; round 6,
+//      measured no faster than the 32x32x16 default).  A wave's output tile of a
+//      column half is its 32 channels x 32 columns as four 16 x 16 sub-tiles n = 2 cb + rb (row
+//      block rb: channels 16 rb .. + 15 of the wave's 32; column block cb: columns 16 cb .. + 15).
+//      Lane (i = lane & 15, q = lane >> 4):
+//        A fragment (weights, slot s = 2 kb + rb of K block kb of 32): A[16 rb + i][32 kb + 8 q + e]
+//        B fragment (image rows, K block kb):                           B[32 kb + 8 q + e][16 cb + i]
+//        accumulator n, element k:                                      D[16 rb + 4 q + k][16 cb + i]
+//      A step (K block kb, column block cb) reads one B fragment pair (hi, lo) and issues 3
+//      products x 2 row blocks: the FLOP, operand registers and LDS bytes of a 32x32x16 step ----
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16(uint4 a, uint4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                   __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+// one 16x16x32 step: 6 MFMAs of 16 cycles, the next steps' B reads after the first pair
+__device__ __forceinline__ void step6_schedule() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);       // 2 MFMAs
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);       // DS reads
+#pragma unroll
+    for (int m = 1; m < 3; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // 2 MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);   // VALU
+        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);   // DS writes
+    }
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // tied no-op: pins a fragment to the accumulator register file (MFMA A operands may be AGPRs)
