@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout) {
     f32x16 acc1[3];
     auto gemm1 = [&](auto j_tag, auto side) {
         constexpr int J = decltype(j_tag)::value;
-        const int row = J < 2 ? Lv[J] : Lh;
+        const int row = J < 2 ? Lv[J < 2 ? J : 0] : Lh;
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc1[J][i] = 0.f;
         uint4 bh[LA + 1], bl[LA + 1];

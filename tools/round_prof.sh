@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-5 evidence on the GPU box: the full default bench (side keys + CPU baseline), the
+# Round evidence on the GPU box: the full default bench (side keys + CPU baseline), the
 # --gatys bench, then rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE passes of both workloads.
-# usage: tools/r5prof.sh <tag>   (then on the build box: python tools/summarize_prof.py ...)
+# usage: tools/round_prof.sh <tag>   (then on the build box: python tools/summarize_prof.py ...)
 set -o pipefail
 TAG=${1:?tag}; shift
 mkdir -p gpurun_out
