@@ -153,17 +153,28 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_s(GramArgs a) {
 // rows 8 g .. + 8 of the fill, g = (l >> 4) + 4 (w >> 2); two fills of loads in flight.
 constexpr int GCN = 8;        // channels per narrow forward workgroup
 constexpr int GFN = 64;       // rows per narrow fill (4 stages)
-__global__ void __launch_bounds__(GWT) k_gram_fwd_n(GramArgs a) {
-    __shared__ __attribute__((aligned(16))) u16 I[(GFN / GSS) * GCN * 32 * FRS];   // [stage][c][u][hi | lo]
-    constexpr int ncg = C / GCN;
+// NFL fills of loads in flight in a ring (round 6; 2 before, with a conditional load that, as in
+// the round-5 wide kernels, made the compiler drain the ring at every fill).  Loads are
+// unconditional: past the chunk a fill re-reads the chunk's last fill (an L2 hit); the loop runs
+// whole rings, the remainder after it.  The MFMA sequence per channel is unchanged (same bits).
+// NC channels per workgroup, one wave each (8; 4 for a single clip: twice the workgroups, 16-B row
+// pieces).  Staging, NC = 8: thread (w, l) loads tensor 8 (w & 3) + (l & 7), channel quad
+// (l >> 3) & 1, rows 8 g .. + 8 of the fill, g = (l >> 4) + 4 (w >> 2); NC = 4: tensor 8 w + (l & 7),
+// channel quad 0, g = l >> 3
+template <int NFL, int NC>
+__global__ void __launch_bounds__(64 * NC) k_gram_fwd_n(GramArgs a) {
+    __shared__ __attribute__((aligned(16))) u16 I[(GFN / GSS) * NC * 32 * FRS];   // [stage][c][u][hi | lo]
+    constexpr int ncg = C / NC;
     const int nwg = a.B * a.nchunk * ncg;
     int work = xcd_remap(blockIdx.x, nwg);
     const int cgi = work % ncg; work /= ncg;
-    const int ch = work % a.nchunk, b = work / a.nchunk, c0 = cgi * GCN;
+    const int ch = work % a.nchunk, b = work / a.nchunk, c0 = cgi * NC;
     const int tlen = a.T / a.nchunk, tbeg = ch * tlen, tend = tbeg + tlen;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int su = 8 * (w & 3) + (lane & 7), sq = (lane >> 3) & 1, g = (lane >> 4) + 4 * (w >> 2);
+    const int su = NC == 8 ? 8 * (w & 3) + (lane & 7) : 8 * w + (lane & 7);
+    const int sq = NC == 8 ? (lane >> 3) & 1 : 0;
+    const int g = NC == 8 ? (lane >> 4) + 4 * (w >> 2) : lane >> 3;
     const bool real = su < a.nu;
     const float* src = real ? (const float*)a.act + (size_t)a.uid[su] * a.tstride +
                               (size_t)b * a.T * C + c0 + 4 * sq + (size_t)8 * g * C
@@ -172,10 +183,11 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_n(GramArgs a) {
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    float4 v[2][8];
+    float4 v[NFL][8];
     auto load = [&](float4 (&vv)[8], int t0) {
+        const int tr = min(t0, tend - GFN);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) vv[k] = *reinterpret_cast<const float4*>(src + (size_t)(t0 + k) * rs);
+        for (int k = 0; k < 8; ++k) vv[k] = *reinterpret_cast<const float4*>(src + (size_t)(tr + k) * rs);
     };
     auto fill = [&](float4 (&vv)[8], int t0) {
         uint4 fh[4], fl[4];
@@ -183,19 +195,19 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_n(GramArgs a) {
         split8<1>(vv, fh[1], fl[1]);
         split8<2>(vv, fh[2], fl[2]);
         split8<3>(vv, fh[3], fl[3]);
-        if (t0 + 2 * GFN < tend) load(vv, t0 + 2 * GFN);
+        load(vv, t0 + NFL * GFN);
         __syncthreads();   // the previous fill's MFMA reads are done
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             // stage g >> 1, channel 4 sq + j, tensor su; rows 8 (g & 1) .. of the stage
-            u16* row = &I[(((g >> 1) * GCN + 4 * sq + j) * 32 + su) * FRS + 8 * (g & 1)];
+            u16* row = &I[(((g >> 1) * NC + 4 * sq + j) * 32 + su) * FRS + 8 * (g & 1)];
             *reinterpret_cast<uint4*>(row) = fh[j];
             *reinterpret_cast<uint4*>(row + 16) = fl[j];
         }
         __syncthreads();
 #pragma unroll
         for (int st = 0; st < GFN / GSS; ++st) {
-            const u16* row = &I[((st * GCN + w) * 32 + r) * FRS + 8 * h];
+            const u16* row = &I[((st * NC + w) * 32 + r) * FRS + 8 * h];
             const uint4 xh = *reinterpret_cast<const uint4*>(row);
             const uint4 xl = *reinterpret_cast<const uint4*>(row + 16);
             acc = mfma_bf16(xh, xh, acc);
@@ -203,12 +215,17 @@ __global__ void __launch_bounds__(GWT) k_gram_fwd_n(GramArgs a) {
             acc = mfma_bf16(xl, xh, acc);
         }
     };
-    load(v[0], tbeg);
-    if (tbeg + GFN < tend) load(v[1], tbeg + GFN);
-    for (int t0 = tbeg; t0 < tend; t0 += 2 * GFN) {
-        fill(v[0], t0);
-        if (t0 + GFN < tend) fill(v[1], t0 + GFN);
+#pragma unroll
+    for (int q = 0; q < NFL; ++q) load(v[q], tbeg + q * GFN);
+    const int nf = tlen / GFN, nring = nf / NFL;
+    int t0 = tbeg;
+    for (int i = 0; i < nring; ++i, t0 += NFL * GFN) {
+#pragma unroll
+        for (int q = 0; q < NFL; ++q) fill(v[q], t0 + q * GFN);
     }
+#pragma unroll
+    for (int q = 0; q < NFL - 1; ++q)
+        if (q < nf - nring * NFL) fill(v[q], t0 + q * GFN);
     float* dst = a.gpart + (((size_t)b * a.nchunk + ch) * C + c0 + w) * 1024;
 #pragma unroll
     for (int i = 0; i < 16; ++i) dst[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = acc[i];
@@ -936,7 +953,23 @@ void launch_gram_fwd_s(const GramArgs& a, hipStream_t s) {
     // 0.28 ms, 8 clips 0.65 -> 0.78 ms, the 32-B row pieces cost more than the extra
     // workgroups return): the 8-channel kernel, same bits
     if ((size_t)a.B * a.nchunk * (C / GCS) < 64 && (a.T / a.nchunk) % GFN == 0) {
-        hipLaunchKernelGGL(k_gram_fwd_n, dim3(a.B * a.nchunk * (C / GCN)), dim3(GWT), 0, s, a);
+        // one clip: 4 channels per workgroup (twice the workgroups) and 3 fills in flight; more
+        // clips: 8 and 2 (round 6, one clip: Gram forward 0.343 -> 0.233 ms, same bits,
+        // profiles/r6_diag/fewclip_ab.txt).  A/B knobs: ASTYLE_GRAM_FWDN_NC (4 / 8),
+        // ASTYLE_GRAM_FWDN_FILLS (2 / 3)
+        static int nfl = -1, ncw = -1;
+        if (nfl < 0) { const char* e = getenv("ASTYLE_GRAM_FWDN_FILLS"); nfl = e ? atoi(e) : 0; }
+        if (ncw < 0) { const char* e = getenv("ASTYLE_GRAM_FWDN_NC"); ncw = e ? atoi(e) : 0; }
+        const int nc = ncw ? ncw : (a.B == 1 ? 4 : 8);
+        const int nf = nfl ? nfl : (nc == 4 ? 3 : 2);
+        const dim3 grid(a.B * a.nchunk * (C / nc));
+        if (nc == 4) {
+            if (nf <= 2) hipLaunchKernelGGL((k_gram_fwd_n<2, 4>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_gram_fwd_n<3, 4>), grid, dim3(256), 0, s, a);
+        } else {
+            if (nf <= 2) hipLaunchKernelGGL((k_gram_fwd_n<2, 8>), grid, dim3(GWT), 0, s, a);
+            else hipLaunchKernelGGL((k_gram_fwd_n<3, 8>), grid, dim3(GWT), 0, s, a);
+        }
         return;
     }
     if (gram_stages() == 2) hipLaunchKernelGGL(k_gram_fwd_s<2>, dim3(a.B * a.nchunk * (C / GCS)), dim3(GWT), 0, s, a);
