@@ -122,8 +122,9 @@ struct ast_ctx {
     size_t esz = 4;                         // bytes per stored element
     void* act = nullptr; size_t tstride = 0;
     void* dgrad = nullptr;   // style-tapped tensors' D out of place (doop; else in place over act)
-    bool doop = false;       // decide_doop / tune_doop: D placement
-    float doop_ms[2] = {-1.f, -1.f};   // tune_doop's Gram-backward times (in place, out of place)
+    bool doop = false;       // decide_doop / timed_gram_bwd: D placement
+    bool doop_tune = false;  // both placements open: the first eager evaluation times them
+    float doop_ms[2] = {-1.f, -1.f};   // that timing's Gram-backward times (in place, out of place)
     uint32_t* mu = nullptr; uint32_t* me = nullptr;
     void* chain[2] = {};
     float* bott = nullptr; float* gbott = nullptr;
@@ -290,18 +291,20 @@ static size_t d_pad() {
 
 int fused_content_occ(const ast_ctx* x);
 
-// ASTYLE_MFMA16=1: the split block kernels on v_mfma_f32_16x16x32_f16 (block_*_split16.hip,
-// round 6: measured no faster); read once per process, since the weight fragments
-// are packed for the kernels that will read them
-static bool mfma16_on() {
+// ASTYLE_MFMA16: the split block kernels on v_mfma_f32_16x16x32_f16 (block_*_split16.hip, round 6:
+// measured): 0 = neither, 1 = forward and backward, 2 = the backward only (default:
+// backward -0.3..-1.2 %, forward +4 % on 16x16x32), 3 = the forward only; read once per process, since the weight fragments are packed for the kernels that will read them
+static int mfma16_mode() {
     static int v = -1;
-    if (v < 0) { const char* e = getenv("ASTYLE_MFMA16"); v = e && atoi(e) ? 1 : 0; }
-    return v == 1;
+    if (v < 0) { const char* e = getenv("ASTYLE_MFMA16"); v = e ? atoi(e) : 2; if (v < 0 || v > 3) v = 2; }
+    return v;
 }
-// (K index kk, output-channel index mm) of element e of lane ln in fragment slot kb of wave w
-// (common.h: the split weight layouts)
-static void frag_index(int kb, int ln, int e, int w, int& kk, int& mm) {
-    if (mfma16_on()) {
+static bool mfma16_fwd() { const int m = mfma16_mode(); return m == 1 || m == 3; }
+static bool mfma16_bwd() { const int m = mfma16_mode(); return m == 1 || m == 2; }
+// (K index kk, output-channel index mm) of element e of lane ln in fragment slot kb of wave w, in
+// the 32x32x16 or (m16) the 16x16x32 layout (common.h: the split weight layouts)
+static void frag_index(bool m16, int kb, int ln, int e, int w, int& kk, int& mm) {
+    if (m16) {
         const int ii = ln & 15, qq = ln >> 4;
         kk = 32 * (kb >> 1) + 8 * qq + e;
         mm = 32 * w + 16 * (kb & 1) + ii;
@@ -357,47 +360,45 @@ GramArgs gram_args(ast_ctx* x);
 GatysArgs gatys_args(ast_ctx* x);
 
 // Where both placements fit (x->dgrad allocated, D at least 4 GiB) and ASTYLE_DOOP does not force
-// one: time the context's own Gram backward (no content tap, no max) on its own buffers in both
-// placements, twice each (in place, out of place, in place, out of place; best of two), and keep
-// the faster, releasing the D buffer when in place wins (by more than 1 %).  The slow in-place
-// mode depends on the physical pages a process got, so it is measured, not
-// guessed: ~90 ms at B = 256, T = 16384.  Results are bit-identical in both placements.
-static int tune_doop(ast_ctx* x) {
-    if (doop_env() >= 0 || !x->dgrad) return 0;
-    const size_t dbytes = (size_t)(x->nblk + 1) * x->tstride * x->esz;
-    if (dbytes < ((size_t)4 << 30)) return 0;
-    hipEvent_t e0, e1;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    float best[2] = {1e30f, 1e30f};
-    for (int rep = 0; rep < 2; ++rep)
-        for (int m = 0; m < 2; ++m) {
-            (void)hipEventRecord(e0, nullptr);
-            if (x->cfg.gatys) {
-                GatysArgs g = gatys_args(x);
-                g.actw = m ? x->dgrad : x->act;
-                launch_gatys_bwd(g, x->split ? 2 : (x->bf ? 1 : 0), nullptr);
-            } else {
-                GramArgs g = gram_args(x);
-                g.actw = m ? x->dgrad : x->act;
-                g.nchunk = x->nchunk_b;
-                launch_gram_bwd_any(x, g, nullptr);
-            }
-            (void)hipEventRecord(e1, nullptr);
-            hipError_t e = hipEventSynchronize(e1);
-            float ms = 0.f;
-            if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-            if (e != hipSuccess) {
-                (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
-                return fail(AST_E_HIP, hipGetErrorString(e));
-            }
-            best[m] = std::min(best[m], ms);
-        }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    x->doop_ms[0] = best[0];
-    x->doop_ms[1] = best[1];
-    if (best[0] < 0.99f * best[1]) {   // in place: give the D buffer back
+// one, the first evaluation that is not being captured into a graph times its own Gram backward in
+// both placements and keeps the faster (in place only when it wins by more than 1 %, releasing the D
+// buffer).  Out of place runs first: it reads E and writes D to its own buffer, so E is still there
+// for the in-place run, which writes the same D over E; either way D is where the chosen placement
+// reads it, and the content tap's partials and the chain's max come out the same (slot stores,
+// atomic max of identical values).  The slow in-place mode depends on the physical pages a process
+// got and on the data, so it is measured on the run's own data (round 6; a timing
+// at create on the empty buffers mispredicted by up to 1 ms).  A capture before that evaluation
+// fixes out of place (a graph holds the D buffer's address).  ~45 ms once at B = 256.
+static bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) { (void)hipGetLastError(); return true; }
+    return st != hipStreamCaptureStatusNone;
+}
+template <class F>
+static int timed_gram_bwd(ast_ctx* x, F launch, hipStream_t s) {
+    if (!x->doop_tune || !x->dgrad) { launch(x->dgrad ? x->dgrad : x->act); return 0; }
+    if (capturing(s)) {   // a graph now holds the out-of-place address: keep it
+        x->doop_tune = false;
+        launch(x->dgrad);
+        return 0;
+    }
+    x->doop_tune = false;
+    hipEvent_t e[3];
+    for (auto& ev : e) HIPCHK(hipEventCreate(&ev));
+    (void)hipEventRecord(e[0], s);
+    launch(x->dgrad);
+    (void)hipEventRecord(e[1], s);
+    launch(x->act);
+    (void)hipEventRecord(e[2], s);
+    hipError_t er = hipEventSynchronize(e[2]);
+    float t_out = 0.f, t_in = 0.f;
+    if (er == hipSuccess) er = hipEventElapsedTime(&t_out, e[0], e[1]);
+    if (er == hipSuccess) er = hipEventElapsedTime(&t_in, e[1], e[2]);
+    for (auto& ev : e) (void)hipEventDestroy(ev);
+    if (er != hipSuccess) return fail(AST_E_HIP, hipGetErrorString(er));
+    x->doop_ms[0] = t_in;
+    x->doop_ms[1] = t_out;
+    if (t_in < 0.99f * t_out) {   // in place: D is over E now; give the D buffer back
         void* base = (char*)x->dgrad - d_pad();
         auto it = std::find(x->allocs.begin(), x->allocs.end(), base);
         if (it != x->allocs.end()) {
@@ -479,7 +480,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
             a.wdn = x->wdn[l]; a.bdm = x->bdm[l];
             a.cus = x->cus;
             a.xin = l == 0 ? xd : nullptr; a.w0 = x->wts + W0_OFF; a.b0 = x->wts + B0_OFF;
-            if (mfma16_on()) launch_block_fwd_s16(a, s);
+            if (mfma16_fwd()) launch_block_fwd_s16(a, s);
             else launch_block_fwd_s(a, s);
         } else if (x->bf) {
             FwdArgsC a;
@@ -803,7 +804,8 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
         if (e != hipSuccess) { ast_destroy(x); return fail(AST_E_HIP, hipGetErrorString(e)); }
     }
 #undef ALLOC
-    if ((rc = tune_doop(x))) { ast_destroy(x); return rc; }
+    x->doop_tune = doop_env() < 0 && x->dgrad &&
+                   (size_t)(x->nblk + 1) * x->tstride * x->esz >= ((size_t)4 << 30);
     *out = x;
     return 0;
 }
@@ -880,11 +882,12 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                         for (int kb = 0; kb < 8; ++kb)
                             for (int ln = 0; ln < 64; ++ln)
                                 for (int e = 0; e < 8; ++e) {
-                                    int kk, mm;
-                                    frag_index(kb, ln, e, w, kk, mm);
+                                    int kk, mm, kb2, mb2;
+                                    frag_index(mfma16_fwd(), kb, ln, e, w, kk, mm);
+                                    frag_index(mfma16_bwd(), kb, ln, e, w, kb2, mb2);
                                     const size_t o = ((((size_t)(w * 3 + tp) * 8 + kb) * 2) * 64 + ln) * 8 + e;
                                     split_half(host[(size_t)tp * C * C + kk * C + mm], k, f[o], f[o + 64 * 8]);
-                                    split_half(host[(size_t)tp * C * C + mm * C + kk], k, g[o], g[o + 64 * 8]);
+                                    split_half(host[(size_t)tp * C * C + mb2 * C + kb2], k, g[o], g[o + 64 * 8]);
                                 }
                 uint4* ds = x->wtss + (size_t)(l - 1) * SBLK;
                 HIPCHK(hipMemcpy(ds + SWDF, f.data(), f.size() * 2, hipMemcpyHostToDevice));
@@ -941,11 +944,12 @@ int ast_set_weight(ast_ctx* x, const char* name, const float* host, size_t n) {
                     for (int kb = 0; kb < 8; ++kb)
                         for (int ln = 0; ln < 64; ++ln)
                             for (int e = 0; e < 8; ++e) {
-                                int kk, mm;
-                                frag_index(kb, ln, e, w, kk, mm);
+                                int kk, mm, kb2, mb2;
+                                frag_index(mfma16_fwd(), kb, ln, e, w, kk, mm);
+                                frag_index(mfma16_bwd(), kb, ln, e, w, kb2, mb2);
                                 const size_t o = ((((size_t)w * 8 + kb) * 2) * 64 + ln) * 8 + e;
                                 split_half(host[(size_t)kk * C + mm], k, f[o], f[o + 64 * 8]);
-                                split_half(host[(size_t)mm * C + kk], k, g[o], g[o + 64 * 8]);
+                                split_half(host[(size_t)mb2 * C + kb2], k, g[o], g[o + 64 * 8]);
                             }
                 uint4* ds = x->wtss + (size_t)(l - 1) * SBLK;
                 HIPCHK(hipMemcpy(ds + SWRF, f.data(), f.size() * 2, hipMemcpyHostToDevice));
@@ -1104,7 +1108,8 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
             g.cont_ncc = x->ncc; g.cont_off = o.off; g.cont_ncol = o.ncol; g.cont_coef = ccoef;
             g.cont_part = x->cpart; g.cont_pstride = (size_t)x->ncpart;
         }
-        launch_gatys_bwd(g, x->split ? 2 : (x->bf ? 1 : 0), s);
+        if ((rc = timed_gram_bwd(x, [&](void* dst) { GatysArgs gg = g; gg.actw = dst; launch_gatys_bwd(gg, x->split ? 2 : (x->bf ? 1 : 0), s); }, s)))
+            return rc;
     } else {
         GramArgs g = gram_args(x);
         launch_gram_fwd_any(x, g, s);
@@ -1130,7 +1135,8 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
             g.cont_part = x->cpart; g.cont_pstride = (size_t)x->ncpart;
         }
         g.nchunk = x->nchunk_b;
-        launch_gram_bwd_any(x, g, s);
+        if ((rc = timed_gram_bwd(x, [&](void* dst) { GramArgs gg = g; gg.actw = dst; launch_gram_bwd_any(x, gg, s); }, s)))
+            return rc;
     }
     tmark(x, s);
     x->lg_front_done = true;
@@ -1180,7 +1186,7 @@ static int loss_grad_back(ast_ctx* x, const float* xd, float* grad, float* parts
             // block 0: the start conv's backward folded in; chain[0] holds the wave partials
             a.w0 = x->wts + W0_OFF;
             a.spart = l == 0 ? (float*)x->chain[0] : nullptr;
-            if (mfma16_on()) launch_block_bwd_s16(a, s);
+            if (mfma16_bwd()) launch_block_bwd_s16(a, s);
             else launch_block_bwd_s(a, s);
         } else if (x->bf) {
             // the bf16 chain holds d loss / d e_l with D_l already added (the kernel adds it)

@@ -75,13 +75,14 @@ void ast_destroy(ast_ctx* ctx);
  * puts the style-tapped tensors' direct loss gradients D: a buffer of their own (one more
  * activation set) when the workspace with it leaves max(16 GiB, 10 %) of the device free (this
  * query and ast_create decide so from the current device's free memory), else in place over the
- * activations.  Where both fit and D is >= 4 GiB, ast_create then times the context's Gram
- * backward in both placements and keeps the faster (releasing the buffer when in place wins), so
- * the query is the upper bound.  Env ASTYLE_DOOP=1 / 0 forces either.  Results are bit-identical
- * in both. */
+ * activations.  Where both fit and D is >= 4 GiB, the context's first evaluation that is not
+ * being captured into a graph (ast_loss_grad / _phase) times its Gram backward in both placements
+ * on its own data and keeps the faster (releasing the buffer when in place wins; a capture before
+ * it keeps out of place), so the query is the upper bound.  Env ASTYLE_DOOP=1 / 0 forces either.
+ * Results are bit-identical in both. */
 int ast_workspace_bytes(const ast_cfg* cfg, size_t* out_bytes);
 /* *out = 1 when the context keeps D out of place (above), 0 when in place; tuned_ms (may be
- * NULL) [2] = the create-time Gram-backward times in place / out of place (-1: not timed).  No
+ * NULL) [2] = the timed Gram backward in place / out of place (-1: not (yet) timed).  No
  * reference counterpart (a memory-placement report). */
 int ast_d_out_of_place(const ast_ctx* ctx, int* out, float* tuned_ms);
 

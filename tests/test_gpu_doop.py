@@ -59,15 +59,22 @@ def test_gram_backward_half_rows_equals_quarter_rows(tmp_path):
 PLACE = r'''
 import os, sys, json, torch
 sys.path.insert(0, sys.argv[1])
+import bench
 from audio_style_transfer_amd.engine import StyleEngine
+dev = torch.device('cuda', 0)
 res = {}
 for gatys in (0, 1):
-    # D of 31 x 32 x 16384 x 128 fp32 = 8 GiB: ast_create times both placements
-    e = StyleEngine(32, 16384, [29], list(range(30)), precision='split',
-                    device=torch.device('cuda', 0), lambd=100.0, gatys=bool(gatys))
-    res[gatys] = e.d_out_of_place(with_times=True)
+    # D of 31 x 32 x 16384 x 128 fp32 = 8 GiB: the first evaluation times both placements
+    e = StyleEngine(32, 16384, [29], list(range(30)), precision='split', device=dev, lambd=100.0,
+                    gatys=bool(gatys))
+    before = e.d_out_of_place(with_times=True)
+    x = bench.make_problem(e, list(range(32)), 16384, dev)
+    p1, g1 = e.loss_grad(x)          # (times both, keeps the faster)
+    p2, g2 = e.loss_grad(x)          # (the chosen placement alone)
+    res[gatys] = {'before': before, 'after': e.d_out_of_place(with_times=True),
+                  'same': bool(torch.equal(p1, p2) and torch.equal(g1, g2))}
     e.close()
-small = StyleEngine(1, 4096, [29], list(range(30)), precision='split', device=torch.device('cuda', 0))
+small = StyleEngine(1, 4096, [29], list(range(30)), precision='split', device=dev)
 res['small'] = small.d_out_of_place(with_times=True)
 small.close()
 print(json.dumps(res))
@@ -75,9 +82,10 @@ print(json.dumps(res))
 
 
 def test_default_placement_is_the_timed_faster_one(tmp_path):
-    """Round 6 default: D out of place where it fits, and where both fit and
-    D is >= 4 GiB, ast_create times the context's Gram backward in both placements and keeps the
-    faster (in place only when it wins by > 1 %).  A small context is not timed (out of place)."""
+    """Round 6 default: D out of place where it fits; where both fit and D is
+    >= 4 GiB, the first evaluation times its Gram backward in both placements on its own data and
+    keeps the faster (in place only when it wins by > 1 %), with the same results as the next
+    evaluation in the chosen placement alone.  A small context is not timed (out of place)."""
     import json
     env = {k: v for k, v in os.environ.items() if k != 'ASTYLE_DOOP'}
     r = subprocess.run([sys.executable, '-c', PLACE, ROOT], env=env, capture_output=True,
@@ -85,8 +93,11 @@ def test_default_placement_is_the_timed_faster_one(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     for k in ('0', '1'):
-        flag, (t_in, t_out) = res[k]
+        flag0, (b_in, b_out) = res[k]['before']
+        assert flag0 and b_in < 0 and b_out < 0, res     # not timed before the first evaluation
+        flag, (t_in, t_out) = res[k]['after']
         assert t_in > 0 and t_out > 0, res
         assert flag == (not t_in < 0.99 * t_out), res
+        assert res[k]['same'], res
     flag, (t_in, t_out) = res['small']
     assert flag and t_in < 0 and t_out < 0, res

@@ -1,6 +1,7 @@
-"""GPU: the 16x16x32 form of the split block kernels (ASTYLE_MFMA16=1, block_fwd_split16.hip /
-block_bwd_split16.hip, round 6): the golden loss / gradient against the fp64 oracle at the split
-mode's bars, agreement with the default 32x32x16 kernels to fp32 rounding (the K accumulation
+"""GPU: the 16x16x32 form of the split block kernels (ASTYLE_MFMA16=1 both, block_fwd_split16.hip /
+block_bwd_split16.hip, round 6; the default 2 runs the backward on it, the forward on 32x32x16):
+the golden loss / gradient against the fp64 oracle at the split mode's bars, agreement with the
+32x32x16 kernels (ASTYLE_MFMA16=0) to fp32 rounding (the K accumulation
 order differs, so not bit for bit), and bit-exact batch invariance (a clip alone equals the same
 clip in slot 2 of 4).  The knob is read once per process, so each setting runs in a child."""
 import json
