@@ -322,6 +322,16 @@ def lib_sha16():
         return None
 
 
+def mfma16_mode():
+    """ASTYLE_MFMA16 as the library reads it (api.hip mfma16_mode): which split block kernels run
+    on 16x16x32 fragments -- 0 neither, 1 both, 2 the backward (default), 3 the forward."""
+    try:
+        v = int(os.environ.get('ASTYLE_MFMA16', '2'))
+    except ValueError:
+        v = 0   # (atoi of a non-number)
+    return v if 0 <= v <= 3 else 2
+
+
 def block_roofline(precision, B, T, fwd_ms, bwd_ms, traffic, ms_per_step, gram_ms, L=30,
                    nblk=30, B_step=None):
     """Roofline of the block kernels.  Per launch (all B clips): algorithmic bytes
@@ -355,8 +365,9 @@ def block_roofline(precision, B, T, fwd_ms, bwd_ms, traffic, ms_per_step, gram_m
         return d
 
     suffix = {'split': '_s', 'bf16': '_c', 'fp32': ''}[precision]
-    f = one('k_block_fwd' + suffix, fwd_ms, fbytes, tf.get('fwd'))
-    b = one('k_block_bwd' + suffix, bwd_ms, bbytes, tf.get('bwd'))
+    m16 = mfma16_mode() if precision == 'split' else 0
+    f = one('k_block_fwd' + suffix + ('16' if m16 in (1, 3) else ''), fwd_ms, fbytes, tf.get('fwd'))
+    b = one('k_block_bwd' + suffix + ('16' if m16 in (1, 2) else ''), bwd_ms, bbytes, tf.get('bwd'))
     dom = b if bwd_ms >= fwd_ms else f
     roof = {k: dom[k] for k in ('bound', 'achieved', 'peak', 'unit', 'frac', 'traffic', 'kernel')}
     roof['note'] = ('dominant kernel (%.1f of %.1f ms/step in the blocks); achieved = algorithmic '
