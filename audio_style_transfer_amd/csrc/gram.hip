@@ -237,31 +237,51 @@ __global__ void __launch_bounds__(256) k_finalize(float* parts, const float* cpa
 // |u| <= wdn max|e_l| + bdm, |W_r tot| <= wrn max|tot|: beyond 2^74 the scaled halves would
 // overflow fp16; below 2^-60 they lose significand bits.
 __global__ void __launch_bounds__(256) k_range_flags(RangeArgs a) {
+    // (round 6: float4 loads, four in flight per thread, and the per-level bound checks spread
+    // over threads; one clip 20 -> ~5 us.  The same flags.)
     const int b = blockIdx.x, tid = threadIdx.x;
-    bool bad = false;
-    for (int i = tid; i < a.T; i += 256) bad |= !isfinite(a.grad[(size_t)b * a.T + i]);
-    if (tid < 4) bad |= !isfinite(a.parts[b * 4 + tid]);
-    bad = __syncthreads_or(bad);
-    if (tid) return;
-    int f = bad ? 1 : 0;
-    if (a.split) {
+    __shared__ int sf;
+    if (tid == 0) sf = 0;
+    int f = 0;
+    const float* g = a.grad + (size_t)b * a.T;
+    if ((a.T & 3) == 0 && (reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+        const float4* g4 = reinterpret_cast<const float4*>(g);
+        const int n4 = a.T >> 2;
+        for (int i = tid; i < n4; i += 4 * 256) {
+            float4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = i + 256 * k < n4 ? g4[i + 256 * k] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (!isfinite(v[k].x) || !isfinite(v[k].y) || !isfinite(v[k].z) || !isfinite(v[k].w)) f = 1;
+        }
+    } else {
+        for (int i = tid; i < a.T; i += 256)
+            if (!isfinite(g[i])) f = 1;
+    }
+    if (tid < 4 && !isfinite(a.parts[b * 4 + tid])) f = 1;
+    if (a.split && tid <= a.nblk) {   // level t = tid of the chain's operand bounds
         const float hi = 0x1p74f, lo = 0x1p-60f;
         auto chk = [&](float m, int bit) {
             if (!(m < hi)) f |= bit;
             else if (m > 0.f && m < lo) f |= 8;
         };
-        for (int t = 0; t <= a.nblk; ++t) {
-            const float ge = __uint_as_float(a.gmax_e[(size_t)t * a.B + b]);
-            const float gg = __uint_as_float(a.gmax_g[(size_t)t * a.B + b]);
-            chk(ge, 2);
-            chk(gg, 4);
-            if (t < a.nblk) {
-                if (!(fmaf(a.wdn[t], ge, a.bdm[t]) < hi)) f |= 2;
-                const float gn = __uint_as_float(a.gmax_g[(size_t)(t + 1) * a.B + b]);
-                if (!(a.wrn[t] * gn < hi)) f |= 4;
-            }
+        const int t = tid;
+        const float ge = __uint_as_float(a.gmax_e[(size_t)t * a.B + b]);
+        const float gg = __uint_as_float(a.gmax_g[(size_t)t * a.B + b]);
+        chk(ge, 2);
+        chk(gg, 4);
+        if (t < a.nblk) {
+            if (!(fmaf(a.wdn[t], ge, a.bdm[t]) < hi)) f |= 2;
+            const float gn = __uint_as_float(a.gmax_g[(size_t)(t + 1) * a.B + b]);
+            if (!(a.wrn[t] * gn < hi)) f |= 4;
         }
     }
+    __syncthreads();
+    if (f) atomicOr(&sf, f);
+    __syncthreads();
+    if (tid) return;
+    f = sf;
     a.flags[b] |= f;   // sticky until ast_range_flags_reset / ast_lbfgs_begin
     a.last[b] = f;     // ast_range_flags_last: this evaluation only
 }
