@@ -148,3 +148,26 @@ def test_kaiser_best_resampler():
     assert y44.shape == (16000,)
     ref = np.sin(2 * np.pi * 440 * np.arange(16000) / 16000)
     assert np.abs(y44[300:-300] - ref[300:-300]).max() <= 4e-3
+
+
+@pytest.mark.parametrize('mode,fwd,bwd', [(None, 'k_block_fwd_s', 'k_block_bwd_s16'),
+                                          ('0', 'k_block_fwd_s', 'k_block_bwd_s'),
+                                          ('1', 'k_block_fwd_s16', 'k_block_bwd_s16'),
+                                          ('3', 'k_block_fwd_s16', 'k_block_bwd_s'),
+                                          ('7', 'k_block_fwd_s', 'k_block_bwd_s16')])
+def test_bench_roofline_names_the_kernels_that_run(monkeypatch, mode, fwd, bwd):
+    """bench.py's roofline names the block kernels ASTYLE_MFMA16 selects, as api.hip's
+    mfma16_mode reads it (default 2: the backward on 16x16x32; out of range -> the default);
+    the roofline arithmetic is the same either way."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    if mode is None:
+        monkeypatch.delenv('ASTYLE_MFMA16', raising=False)
+    else:
+        monkeypatch.setenv('ASTYLE_MFMA16', mode)
+    r = bench.block_roofline('split', 256, 16384, 1.57, 1.67, None, 130.0, 33.0)
+    assert r['fwd']['kernel'] == fwd and r['bwd']['kernel'] == bwd
+    assert r['kernel'] == bwd   # the backward is the longer one
+    assert abs(r['bwd']['algorithmic_bytes'] - (3 * 256 * 16384 * 128 * 4 + 32 * 256 * 16384)) < 1
+    assert bench.block_roofline('bf16', 256, 16384, 1.0, 1.2, None, 50.0, 20.0)['bwd']['kernel'] == 'k_block_bwd_c'
