@@ -21,6 +21,10 @@ namespace {
 
 thread_local std::string g_err;
 unsigned long long* g_stamps = nullptr;   // diagnostic phase stamps (ASTYLE_STAMPS builds)
+static int g_stamp_row = 0;               // block launches since ast_debug_stamps: row of 20 words each
+static unsigned long long* stamp_row() {  // (64 rows; a launch's max / min wave lifetime in its row)
+    return g_stamps ? g_stamps + 20 * (g_stamp_row++ & 63) : nullptr;
+}
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -465,7 +469,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
         uint32_t* me = x->me + (size_t)l * c.batch * c.T * 4;
         if (x->split) {
             FwdArgsS a;
-            a.stamps = g_stamps;
+            a.stamps = stamp_row();
             const uint4* ws = x->wtss + (size_t)l * SBLK;
             a.ein = (const float*)tens(x, l); a.eout = (float*)tens(x, l + 1);
             a.wdf = ws + SWDF; a.wrf = ws + SWRF; a.bd = w + BD; a.br = w + BR;
@@ -484,7 +488,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
             else launch_block_fwd_s(a, s);
         } else if (x->bf) {
             FwdArgsC a;
-            a.stamps = g_stamps;
+            a.stamps = stamp_row();
             u16* wb = blkwb(x, l);
             a.ein = (const u16*)tens(x, l); a.eout = (u16*)tens(x, l + 1);
             a.wf = wb + WFB; a.wrf = wb + WRFB; a.bd = w + BD; a.br = w + BR;
@@ -681,8 +685,9 @@ int ast_ot_admm(const double* p_mod, const double* p_ref, int nprob, int n1, int
 
 // Diagnostic hook (not in astyle.h): device buffer of 12 u64 phase-cycle sums that
 // -DASTYLE_STAMPS builds of the bf16 block kernels accumulate into; NULL disables.
-int ast_debug_stamps(void* dev_u64x16) {
-    g_stamps = (unsigned long long*)dev_u64x16;
+int ast_debug_stamps(void* dev_u64x20x64) {   // 64 rows of 20: [0..15] sums, [16] / [17] max / min wave lifetime, [18] / [19] first start / last end
+    g_stamps = (unsigned long long*)dev_u64x20x64;
+    g_stamp_row = 0;
     return 0;
 }
 
@@ -1169,7 +1174,7 @@ static int loss_grad_back(ast_ctx* x, const float* xd, float* grad, float* parts
         if (x->split) {
             // like the bf16 chain, the chain holds d loss / d e_l with D_l already added
             BwdArgsS a;
-            a.stamps = g_stamps;
+            a.stamps = stamp_row();
             const uint4* ws = x->wtss + (size_t)l * SBLK;
             a.tin = (const float*)(gin ? gin : din);
             a.dadd = l > 0 ? (const float*)direct(l) : nullptr;
@@ -1191,7 +1196,7 @@ static int loss_grad_back(ast_ctx* x, const float* xd, float* grad, float* parts
         } else if (x->bf) {
             // the bf16 chain holds d loss / d e_l with D_l already added (the kernel adds it)
             BwdArgsC a;
-            a.stamps = g_stamps;
+            a.stamps = stamp_row();
             u16* wb = blkwb(x, l);
             a.tin = (const u16*)(gin ? gin : din);
             a.dadd = l > 0 ? (const u16*)direct(l) : nullptr;

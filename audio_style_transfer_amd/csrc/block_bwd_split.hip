@@ -70,6 +70,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout) {
     __shared__ __attribute__((aligned(16))) uint8_t XG[GROWS * RS];   // split g_u image
     __shared__ __attribute__((aligned(16))) uint8_t ER[2][ISLOT];     // fp32 tot + D_l rows
     __shared__ __attribute__((aligned(16))) float W0S[SX ? 3 * C : 4];   // SX: W0 [3][C]
+    __shared__ uint32_t WMX[4];                                     // the drain's per-wave maxima
 
     const int tiles = a.T / TMS;
     const int ntiles = a.B * tiles;
@@ -470,7 +471,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout) {
         epi_begin(prv, 1);
 #pragma unroll
         for (int q = 0; q < 12; ++q) epi_part(1, q / 3, q % 3, erl, me_p, inv2p);
-        epi_max(prv.b);
+        wg_max_flush(WMX, wave_max_bits(omax), a.gmax_out + prv.b);
     }
     STAMP(12)
     STAMP_FLUSH(a.stamps)

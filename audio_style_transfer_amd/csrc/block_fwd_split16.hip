@@ -69,6 +69,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s16(FwdArgsS a, Layout) {
     __shared__ __attribute__((aligned(16))) uint16_t MBU[TMS * 8];  // u > 0 words of the tile
     __shared__ __attribute__((aligned(16))) uint16_t MBE[TMS * 8];  // e_{l+1} > 0 words
     __shared__ int MBT[TMS];                                        // time of each tile column
+    __shared__ uint32_t WMX[4];                                     // the drain's per-wave maxima
 
     const int tiles = a.T / TMS;
     const int ntiles = a.B * tiles;
@@ -510,8 +511,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s16(FwdArgsS a, Layout) {
             flush_part(q >> 2, q & 3, 1, erl);
         }
         epi2_words();
-        epi2_max();
-        lds_barrier();
+        wg_max_flush(WMX, wave_max_bits(emax), a.gmax_out + prv.b);   // (its barrier: the e > 0 words too)
         store_me(prv.b);
     }
     STAMP(4)

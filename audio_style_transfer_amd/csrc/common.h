@@ -43,7 +43,9 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 #define STAMP(k) { const unsigned long long st_t = stamp_now(); st_acc[k] += st_t - st_prev; st_prev = st_t; }
 #define STAMP_FLUSH(ptr) if (((threadIdx.x & 63) == 0) && (ptr)) { \
     st_acc[15] = __builtin_amdgcn_s_memrealtime() - st_rt0; \
-    for (int k = 0; k < 16; ++k) atomicAdd(&(ptr)[k], st_acc[k]); }
+    for (int k = 0; k < 16; ++k) atomicAdd(&(ptr)[k], st_acc[k]); \
+    atomicMax(&(ptr)[16], st_acc[15]); atomicMin(&(ptr)[17], st_acc[15]); \
+    atomicMin(&(ptr)[18], st_rt0); atomicMax(&(ptr)[19], st_rt0 + st_acc[15]); }
 __device__ __forceinline__ unsigned long long stamp_now() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);

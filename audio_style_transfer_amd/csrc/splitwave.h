@@ -348,6 +348,16 @@ __device__ __forceinline__ uint32_t wave_max_bits(float x) {
     return (uint32_t)max(max(a, b), max(c, d));
 }
 
+// The end of a block launch: the workgroup's max for its last clip in ONE global atomic, the four
+// waves' maxima meeting in LDS first (round 6).  At one clip every workgroup ends on the same
+// clip, and the 1024 per-wave atomics on one line serialised at L2 (~8 ns each: ~8 us of a 25-us
+// launch; phase stamps showed the waves done after ~12 us).  The max is the same.
+__device__ __forceinline__ void wg_max_flush(uint32_t (&slots)[4], uint32_t m, unsigned* dst) {
+    if ((threadIdx.x & 63) == 0) slots[threadIdx.x >> 6] = m;
+    lds_barrier();
+    if (threadIdx.x == 0) atomicMax(dst, max(max(slots[0], slots[1]), max(slots[2], slots[3])));
+}
+
 // [x > 0] as 0 / 1 for every non-NaN x: the bits as a signed integer clamped to [0, 1] (one
 // v_med3_i32; +0 and negatives give 0)
 __device__ __forceinline__ uint32_t pos_bit(float x) {

@@ -28,13 +28,15 @@ def stamps(top):
     eng.set_targets(torch.randn(T, 128) * 0.1, torch.randn(*eng.style_shape) * 0.01)
     eng.loss_grad(x)
     torch.cuda.synchronize()
-    buf = torch.zeros(16, dtype=torch.int64, device='cuda')
+    buf = torch.zeros(64, 20, dtype=torch.int64, device='cuda')   # a row per block launch
+    buf[:, 17] = 2 ** 62   # (the min wave lifetime slots)
+    buf[:, 18] = 2 ** 62   # (the first wave start slots)
     lib.ast_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
     eng.loss_grad(x)
     torch.cuda.synchronize()
     lib.ast_debug_stamps(None)
     eng.close()
-    return buf.cpu().tolist()
+    return buf[:, :16].sum(dim=0).cpu().tolist()
 
 
 tiles = B * T // 64 / 256   # tiles per CU of one launch

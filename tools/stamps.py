@@ -20,13 +20,31 @@ if mode == 'bwd':
     eng.set_targets(torch.randn(T, 128) * 0.1, torch.randn(*eng.style_shape) * 0.01)
 run = (lambda: eng.loss_grad(x)) if mode == 'bwd' else (lambda: eng.forward(x))
 run(); torch.cuda.synchronize()
-buf = torch.zeros(16, dtype=torch.int64, device='cuda')
+buf = torch.zeros(64, 20, dtype=torch.int64, device='cuda')   # a row per block launch
+buf[:, 17] = 2 ** 62   # (the min wave lifetime slots)
+buf[:, 18] = 2 ** 62   # (the first wave start slots)
 lib = _lib.load()
 lib.ast_debug_stamps.argtypes = [ctypes.c_void_p]
 lib.ast_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
-run(); torch.cuda.synchronize()
-lib.ast_debug_stamps(None)
-v = buf.cpu().tolist()
+if os.environ.get('STAMPS_GRAPH', '0') != '0':
+    # captured (the stamp rows are baked into the kernels' arguments), then replayed: the
+    # launches run back to back as the bench's graph replays run them
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        run()
+    lib.ast_debug_stamps(None)
+    g.replay(); torch.cuda.synchronize()   # (warm)
+    buf.zero_(); buf[:, 17] = 2 ** 62; buf[:, 18] = 2 ** 62
+    g.replay(); torch.cuda.synchronize()
+else:
+    run(); torch.cuda.synchronize()
+    lib.ast_debug_stamps(None)
+rows = buf.cpu().tolist()
+v = [sum(r[k] for r in rows) for k in range(16)]
+launched = [r for r in rows if r[15]]   # per launch: max / min wave lifetime
+v += [sum(r[16] for r in launched) / max(len(launched), 1), sum(r[17] for r in launched) / max(len(launched), 1)]
 if prec == 'bf16':
     names = ['fwd: top wait + barrier', 'fwd: GEMM1 + epi2 of prev + DMA', 'fwd: epi1 + GEMM2', '-',
              'bwd: top wait + barrier', 'bwd: step 1 + g_u + barrier', 'bwd: step 2 + DMA',
@@ -67,6 +85,11 @@ else:
     if v[15]:   # wave lifetimes in 100-MHz ticks: the clock the kernels ran at
         cyc = sum(v[k] for k in range(15))
         print('%-48s %8.0f MHz (shader cycles / s_memrealtime ticks, all stamped kernels)' % ('effective clock', 100.0 * cyc / v[15]))
+        print('%-48s mean %.2f  per launch: max %.2f  min %.2f us (averaged over %d launches)' % (
+            'wave lifetime', v[15] / (4 * 256 * len(launched)) / 100.0, v[16] / 100.0, v[17] / 100.0, len(launched)))
+        for i, r in enumerate(launched):
+            print('   launch %2d: wave lifetime max %.2f  min %.2f us; first start -> last end %.2f us; gap after the previous launch %.2f us' % (
+                i, r[16] / 100.0, r[17] / 100.0, (r[19] - r[18]) / 100.0, (r[18] - launched[i - 1][19]) / 100.0 if i else 0.0))
     sys.exit(0)
 for lo, hi in groups:
     tot = sum(v[lo:hi])
