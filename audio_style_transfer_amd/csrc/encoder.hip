@@ -366,8 +366,13 @@ __global__ void __launch_bounds__(256) k_startconv_masks(const float* __restrict
     }
     *reinterpret_cast<uint4*>(me0 + rowi * 8) =
         make_uint4((uint32_t)P0, (uint32_t)(P0 >> 32), (uint32_t)P1, (uint32_t)(P1 >> 32));
+    // the workgroup's max in one atomic (at one clip, 64 workgroups x 4 waves on one line otherwise)
+    __shared__ float wmx[4];
     amax = wave_max_f(amax);
-    if ((threadIdx.x & 63) == 0) atomicMax(gmax + blockIdx.x % B, __float_as_uint(amax));
+    if ((threadIdx.x & 63) == 0) wmx[threadIdx.x >> 6] = amax;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        atomicMax(gmax + blockIdx.x % B, __float_as_uint(fmaxf(fmaxf(wmx[0], wmx[1]), fmaxf(wmx[2], wmx[3]))));
 }
 
 // d loss / d x (startconv transposed, model.py:82-93, incl. the 1/128 of model.py:83):
