@@ -121,8 +121,8 @@ struct ast_ctx {
     float wdn[NBLK_MAX] = {}, wrn[NBLK_MAX] = {}, bdm[NBLK_MAX] = {};   // operand bounds (splitwave.h)
     bool bf = false;                        // precision 1: bf16 activations/gradients
     bool split = false;                     // precision 2: fp32 storage, split-fp16 block GEMMs
-    unsigned* gmax_e = nullptr;             // [nblk + 1][B] max |e_l| per clip (precision 2)
-    unsigned* gmax_g = nullptr;             // [nblk + 1][B] max |d loss / d e_l| per clip
+    unsigned* gmax_e = nullptr;             // [nblk + 1][B][GCLIP_W] max |e_l| per clip, in slots (precision 2)
+    unsigned* gmax_g = nullptr;             // [nblk + 1][B][GCLIP_W] max |d loss / d e_l| per clip
     size_t esz = 4;                         // bytes per stored element
     void* act = nullptr; size_t tstride = 0;
     void* dgrad = nullptr;   // style-tapped tensors' D out of place (doop; else in place over act)
@@ -323,7 +323,7 @@ size_t workspace_bytes(const ast_cfg* c, const ast_ctx* x) {
     const size_t es = c->precision == 1 ? 2 : 4;
     size_t n = 0;
     n += W_TOTAL * 4 + (size_t)NBLK_MAX * BLKB_SZ * 2;
-    if (c->precision == 2) n += (size_t)NBLK_MAX * SBLK * 16 + 2 * (size_t)(NBLK_MAX + 1) * c->batch * 4;
+    if (c->precision == 2) n += (size_t)NBLK_MAX * SBLK * 16 + 2 * (size_t)(NBLK_MAX + 1) * c->batch * GCLIP_W * 4;
     n += (size_t)(x->nblk + 1) * (BTC + tensor_pad()) * es * (x->doop ? 2 : 1);   // act (+ D)
     if (x->doop) n += d_pad();
     n += 2 * (size_t)x->nblk * c->batch * c->T * 16;        // mu, me
@@ -455,7 +455,7 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
     x->lg_front_done = false;   // phase 1's state (act, gmax) is about to be overwritten
     const ast_cfg& c = x->cfg;
     if (x->split) {
-        launch_zero32(x->gmax_e, (size_t)(NBLK_MAX + 1) * c.batch * 4, s, 0);
+        launch_zero32(x->gmax_e, (size_t)(NBLK_MAX + 1) * c.batch * GCLIP_W * 4, s, 0);
         // e_0 is not stored: block 0 recomputes it from x (FwdArgsS::xin); masks and max only
         launch_startconv_masks((const float*)xd, x->wts + W0_OFF, x->wts + B0_OFF, c.batch, c.T, s,
                                (uint16_t*)x->me, x->gmax_e);
@@ -475,8 +475,8 @@ int run_forward(ast_ctx* x, const float* xd, hipStream_t s, bool mark = false) {
             a.wdf = ws + SWDF; a.wrf = ws + SWRF; a.bd = w + BD; a.br = w + BR;
             a.mu = (uint16_t*)mu;
             a.me_next = l + 1 < x->nblk ? (uint16_t*)(me + (size_t)c.batch * c.T * 4) : nullptr;
-            a.gmax_in = (const float*)(x->gmax_e + (size_t)l * c.batch);
-            a.gmax_out = x->gmax_e + (size_t)(l + 1) * c.batch;
+            a.gmax_in = (const float*)(x->gmax_e + (size_t)l * c.batch * GCLIP_W);
+            a.gmax_out = x->gmax_e + (size_t)(l + 1) * c.batch * GCLIP_W;
             a.zero = (const float*)x->zero;
             a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
             a.dn_log2 = (l + 1) % 10; a.nn = c.T >> a.dn_log2;
@@ -764,8 +764,8 @@ int ast_create(const ast_cfg* cfg, int hip_device, ast_ctx** out) {
     if (x->split) {
         ALLOC(x->wtss, (size_t)NBLK_MAX * SBLK * 16);
         (void)hipMemset(x->wtss, 0, (size_t)NBLK_MAX * SBLK * 16);
-        ALLOC(x->gmax_e, (size_t)(NBLK_MAX + 1) * c.batch * 4);
-        ALLOC(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4);
+        ALLOC(x->gmax_e, (size_t)(NBLK_MAX + 1) * c.batch * GCLIP_W * 4);
+        ALLOC(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * GCLIP_W * 4);
     }
     ALLOC(x->wts, W_TOTAL * 4);
     (void)hipMemset(x->wts, 0, W_TOTAL * 4);
@@ -1101,8 +1101,8 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
         tmark(x, s);
         if (x->split && x->tensor_in_style[x->nblk]) {   // the chain's first max |tot| inside the Gatys bwd
             for (int u = 0; u < x->nu; ++u) if (x->uid[u] == x->nblk) g.top_u = u;
-            g.gmax_top = x->gmax_g + (size_t)x->nblk * c.batch;
-            launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s, 2);
+            g.gmax_top = x->gmax_g + (size_t)x->nblk * c.batch * GCLIP_W;
+            launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * GCLIP_W * 4, s, 2);
             top_max_done = g.top_u >= 0;
         }
         if (fuse_u >= 0) {   // the split Gatys backward adds the content tap (one slot per 512-row tile)
@@ -1127,8 +1127,8 @@ static int loss_grad_front(ast_ctx* x, const float* xd, hipStream_t s) {
         tmark(x, s);
         if (x->split && x->tensor_in_style[x->nblk]) {   // the chain's first max |tot| inside the Gram bwd
             for (int u = 0; u < x->nu; ++u) if (x->uid[u] == x->nblk) g.top_u = u;
-            g.gmax_top = x->gmax_g + (size_t)x->nblk * c.batch;
-            launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s, 2);
+            g.gmax_top = x->gmax_g + (size_t)x->nblk * c.batch * GCLIP_W;
+            launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * GCLIP_W * 4, s, 2);
             top_max_done = g.top_u >= 0;
         }
         if (fuse_u >= 0) {
@@ -1158,10 +1158,10 @@ static int loss_grad_back(ast_ctx* x, const float* xd, float* grad, float* parts
         return x->tensor_in_style[t] ? (x->dgrad ? (const void*)((char*)x->dgrad + (size_t)t * x->tstride * x->esz) : tens(x, t)) : x->cg_buf[t];
     };
     if (x->split && !top_max_done) {
-        launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * 4, s, 2);
+        launch_zero32(x->gmax_g, (size_t)(NBLK_MAX + 1) * c.batch * GCLIP_W * 4, s, 2);
         const void* top = direct(x->nblk);
         if (!top) return fail(AST_E_STATE, "top block has no loss gradient");
-        launch_absmax((const float*)top, (size_t)c.T * C, c.batch, x->gmax_g + (size_t)x->nblk * c.batch, s);
+        launch_absmax((const float*)top, (size_t)c.T * C, c.batch, x->gmax_g + (size_t)x->nblk * c.batch * GCLIP_W, s);
     }
     for (int l = x->nblk - 1; l >= 0; --l) {
         float* w = blkw(x, l);
@@ -1181,8 +1181,8 @@ static int loss_grad_back(ast_ctx* x, const float* xd, float* grad, float* parts
             a.gout = (float*)x->chain[l & 1];
             a.wrb = ws + SWRB; a.wdb = ws + SWDB;
             a.mu = (const uint16_t*)mu; a.me = (const uint16_t*)me;
-            a.gmax_in = (const float*)(x->gmax_g + (size_t)(l + 1) * c.batch);
-            a.gmax_out = x->gmax_g + (size_t)l * c.batch;
+            a.gmax_in = (const float*)(x->gmax_g + (size_t)(l + 1) * c.batch * GCLIP_W);
+            a.gmax_out = x->gmax_g + (size_t)l * c.batch * GCLIP_W;
             a.zero = (const float*)x->zero;
             a.B = c.batch; a.T = c.T; a.d = d; a.n = c.T / d;
             a.kd = x->kd[l]; a.kr = x->kr[l];

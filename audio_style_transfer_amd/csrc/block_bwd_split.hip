@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout) {
     };
     auto epi_max = [&](int b) {
         const uint32_t m = wave_max_bits(omax);
-        if (lane == 0) atomicMax(a.gmax_out + b, m);
+        if (lane == 0) atomicMax(gslot(a.gmax_out, b, blockIdx.x), m);
         omax = 0.f;
     };
     using J0 = std::integral_constant<int, 0>;
@@ -358,7 +358,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout) {
         for (int k = 0; k < NU; ++k) load_unit(t0, k);
         load_masks(t0, mu_c, muh_c, me_c);
         const uint32_t z0 = zbits(t0);
-        gm_c = sload(a.gmax_in + t0.b);
+        gm_c = sload_gmax(a.gmax_in, t0.b);
         const float s0 = exp2i(scale_exp(gm_c));
 #pragma unroll
         for (int k = 0; k < NU; ++k) conv_unit(k, &ER[0][0], s0, z0);
@@ -384,7 +384,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout) {
         const int m_u = scale_exp(a.wrn * gm);
         const float f_u = exp2i(m_u - m_t - a.kr);   // acc units 2^(m_t + k_r) -> g_u 2^m_u
         const float inv2 = exp2i(-(m_u + a.kd));
-        if (nt.b != cu.b) gm_c = sload(a.gmax_in + nt.b);   // (usually the same clip: tile order)
+        if (nt.b != cu.b) gm_c = sload_gmax(a.gmax_in, nt.b);   // (usually the same clip: tile order)
         const float s_next = exp2i(scale_exp(gm_c));
         const uint32_t zn = zbits(nt);
         uint8_t* erc = &ER[it & 1][0];          // this tile's residual
@@ -471,7 +471,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_bwd_s(BwdArgsS a, Layout) {
         epi_begin(prv, 1);
 #pragma unroll
         for (int q = 0; q < 12; ++q) epi_part(1, q / 3, q % 3, erl, me_p, inv2p);
-        wg_max_flush(WMX, wave_max_bits(omax), a.gmax_out + prv.b);
+        wg_max_flush(WMX, wave_max_bits(omax), gslot(a.gmax_out, prv.b, blockIdx.x));
     }
     STAMP(12)
     STAMP_FLUSH(a.stamps)
@@ -489,7 +489,7 @@ __global__ void __launch_bounds__(256) k_absmax(const float* __restrict__ x, siz
         m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
     m = wave_max(m);
-    if ((threadIdx.x & 63) == 0) atomicMax(out + b, __float_as_uint(m));
+    if ((threadIdx.x & 63) == 0) atomicMax(gslot(out, b, blockIdx.x), __float_as_uint(m));
 }
 
 }  // namespace

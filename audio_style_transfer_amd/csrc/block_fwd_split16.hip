@@ -279,7 +279,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s16(FwdArgsS a, Layout) {
     // clip-interleaved tile order a workgroup usually keeps its clip for the whole launch)
     auto epi2_max = [&]() {
         const uint32_t m = wave_max_bits(emax);
-        if (lane == 0) atomicMax(a.gmax_out + prv.b, m);
+        if (lane == 0) atomicMax(gslot(a.gmax_out, prv.b, blockIdx.x), m);
         emax = 0.f;
     };
 
@@ -422,7 +422,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s16(FwdArgsS a, Layout) {
 #pragma unroll
         for (int k = 0; k < NU; ++k) load_unit(t0, k);
         const uint32_t z0 = zero_bits_of(t0);
-        gm_c = sload(a.gmax_in + t0.b);
+        gm_c = sload_gmax(a.gmax_in, t0.b);
         const float s0 = exp2i(scale_exp(gm_c));
 #pragma unroll
         for (int k = 0; k < NU; ++k) conv_unit(k, &ER[0][0], s0, z0);
@@ -442,7 +442,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s16(FwdArgsS a, Layout) {
         const float gm = gm_c;
         const int m_e = scale_exp(gm);
         const int m_v = scale_exp(fmaf(a.wdn, gm, a.bdm));
-        if (nt.b != cu.b) gm_c = sload(a.gmax_in + nt.b);   // (usually the same clip: tile order)
+        if (nt.b != cu.b) gm_c = sload_gmax(a.gmax_in, nt.b);   // (usually the same clip: tile order)
         const float s_next = exp2i(scale_exp(gm_c));
         const uint32_t zn = zero_bits_of(nt);
         const float sv = exp2i(m_v);
@@ -511,7 +511,7 @@ __global__ void __launch_bounds__(FT, 1) k_block_fwd_s16(FwdArgsS a, Layout) {
             flush_part(q >> 2, q & 3, 1, erl);
         }
         epi2_words();
-        wg_max_flush(WMX, wave_max_bits(emax), a.gmax_out + prv.b);   // (its barrier: the e > 0 words too)
+        wg_max_flush(WMX, wave_max_bits(emax), gslot(a.gmax_out, prv.b, blockIdx.x));   // (its barrier: the e > 0 words too)
         store_me(prv.b);
     }
     STAMP(4)

@@ -173,7 +173,17 @@ struct BwdArgsC {
 // fragments, slot s = 2 kb + rb (K block kb of 32, row block rb), lane (i, q) = (lane & 15, lane >> 4):
 //   wdf: W_d[tap][32 kb + 8 q + e][32 w + 16 rb + i]     wrf: W_r[32 kb + 8 q + e][32 w + 16 rb + i]
 //   wrb: W_r[32 w + 16 rb + i][32 kb + 8 q + e]          wdb: W_d[tap][32 w + 16 rb + i][32 kb + 8 q + e]
-// gmax_*: per clip max |x| of a tensor as float bits (atomic max of the non-negative bit pattern).
+// gmax_*: per clip max |x| of a tensor as float bits (atomic max of the non-negative bit pattern),
+// in GSLOTS slots per clip, one 128-B line each ([level][clip][slot][32 words], word 0 used): a
+// writer takes slot blockIdx.x % GSLOTS (one per XCD under round-robin placement), a reader the
+// max of the slots (round 6: at one clip every workgroup of a block launch ends on the same clip,
+// and 256 atomics on one line serialised ~2 us per launch).
+constexpr int GSLOTS = 8;
+constexpr int GSLOT_W = 32;                 // words per slot
+constexpr int GCLIP_W = GSLOTS * GSLOT_W;   // words per clip and level
+__host__ __device__ inline unsigned* gslot(unsigned* lvl, int b, unsigned slot) {
+    return lvl + (size_t)b * GCLIP_W + (slot % GSLOTS) * GSLOT_W;
+}
 // Division by a launch-invariant divisor without the signed-division expansion (~17 scalar
 // instructions each): q = mulhi(x, m) >> s with m = ceil(2^(31 + l) / n), 2^l >= n, exact for
 // every 0 <= x < 2^31 (Granlund-Montgomery); n = 1 passes x through.
@@ -364,7 +374,7 @@ void launch_finalize(float* parts, const float* cpart, int ncpart, float cscale,
 // per-clip range / finiteness flags of one loss+grad evaluation (gram.hip, ast_range_flags)
 struct RangeArgs {
     const float* parts; const float* grad;  // [B][4], [B][T]
-    const unsigned* gmax_e; const unsigned* gmax_g;   // split: [nblk + 1][B] per-clip maxima
+    const unsigned* gmax_e; const unsigned* gmax_g;   // split: [nblk + 1][B][GCLIP_W] per-clip maxima
     int split, nblk, B, T;
     float wdn[30], bdm[30], wrn[30];        // split: the per-block operand bounds (splitwave.h)
     int* flags;                             // [B] OR'ed (sticky)

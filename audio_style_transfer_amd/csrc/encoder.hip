@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(256) k_startconv_masks(const float* __restrict
     if ((threadIdx.x & 63) == 0) wmx[threadIdx.x >> 6] = amax;
     __syncthreads();
     if (threadIdx.x == 0)
-        atomicMax(gmax + blockIdx.x % B, __float_as_uint(fmaxf(fmaxf(wmx[0], wmx[1]), fmaxf(wmx[2], wmx[3]))));
+        atomicMax(gslot(gmax, blockIdx.x % B, blockIdx.x), __float_as_uint(fmaxf(fmaxf(wmx[0], wmx[1]), fmaxf(wmx[2], wmx[3]))));
 }
 
 // d loss / d x (startconv transposed, model.py:82-93, incl. the 1/128 of model.py:83):

@@ -267,13 +267,20 @@ __global__ void __launch_bounds__(256) k_range_flags(RangeArgs a) {
             else if (m > 0.f && m < lo) f |= 8;
         };
         const int t = tid;
-        const float ge = __uint_as_float(a.gmax_e[(size_t)t * a.B + b]);
-        const float gg = __uint_as_float(a.gmax_g[(size_t)t * a.B + b]);
+        auto gread = [&](const unsigned* g, int lv) {   // the clip's max over its slots (common.h)
+            const unsigned* p = g + ((size_t)lv * a.B + b) * GCLIP_W;
+            unsigned m = 0;
+#pragma unroll
+            for (int q = 0; q < GSLOTS; ++q) m = max(m, p[q * GSLOT_W]);
+            return __uint_as_float(m);
+        };
+        const float ge = gread(a.gmax_e, t);
+        const float gg = gread(a.gmax_g, t);
         chk(ge, 2);
         chk(gg, 4);
         if (t < a.nblk) {
             if (!(fmaf(a.wdn[t], ge, a.bdm[t]) < hi)) f |= 2;
-            const float gn = __uint_as_float(a.gmax_g[(size_t)(t + 1) * a.B + b]);
+            const float gn = gread(a.gmax_g, t + 1);
             if (!(a.wrn[t] * gn < hi)) f |= 4;
         }
     }

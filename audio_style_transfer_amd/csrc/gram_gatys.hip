@@ -557,7 +557,7 @@ __global__ void __launch_bounds__(256) k_gatys_bwd_s2(GatysArgs a) {
         for (int off = 32; off > 0; off >>= 1) omax = fmaxf(omax, __shfl_xor(omax, off));
         if (lane == 0) mw[w] = omax;
         __syncthreads();
-        if (tid == 0) atomicMax(a.gmax_top + b, __float_as_uint(fmaxf(fmaxf(mw[0], mw[1]), fmaxf(mw[2], mw[3]))));
+        if (tid == 0) atomicMax(gslot(a.gmax_top, b, blockIdx.x), __float_as_uint(fmaxf(fmaxf(mw[0], mw[1]), fmaxf(mw[2], mw[3]))));
     }
     if (cont) {   // the workgroup's squared content error -> slot `tile` (fixed order: waves 0..3)
         __shared__ float cw[4];

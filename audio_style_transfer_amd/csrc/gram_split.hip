@@ -442,7 +442,7 @@ __global__ void __launch_bounds__(GWT) k_gram_bwd_s(GramArgs a) {
             float m = wm[0];
 #pragma unroll
             for (int k = 1; k < GWT / 64; ++k) m = fmaxf(m, wm[k]);
-            atomicMax(a.gmax_top + b, __float_as_uint(m));
+            atomicMax(gslot(a.gmax_top, b, blockIdx.x), __float_as_uint(m));
         }
     }
 }
@@ -658,7 +658,7 @@ __global__ void __launch_bounds__(HWT) k_gram_bwd_h(GramArgs a) {
             float m = wm[0];
 #pragma unroll
             for (int k = 1; k < HWT / 64; ++k) m = fmaxf(m, wm[k]);
-            atomicMax(a.gmax_top + b, __float_as_uint(m));
+            atomicMax(gslot(a.gmax_top, b, blockIdx.x), __float_as_uint(m));
         }
     }
 }

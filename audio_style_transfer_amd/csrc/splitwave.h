@@ -315,6 +315,22 @@ __device__ __forceinline__ float sload(const float* p) {
     return v;
 }
 
+// a clip's max over its GSLOTS slots (common.h): eight scalar loads in flight, one wait.  The
+// outputs are early-clobber: a load's destination must not be the base pair the later loads read
+__device__ __forceinline__ float sload_gmax(const float* lvl, int b) {
+    const float* p = lvl + (size_t)b * GCLIP_W;
+    uint32_t v0, v1, v2, v3, v4, v5, v6, v7;
+    static_assert(GSLOTS == 8 && GSLOT_W == 32, "sload_gmax: 8 slots 128 B apart");
+    asm volatile("s_load_dword %0, %8, 0x0\n\ts_load_dword %1, %8, 0x80\n\t"
+                 "s_load_dword %2, %8, 0x100\n\ts_load_dword %3, %8, 0x180\n\t"
+                 "s_load_dword %4, %8, 0x200\n\ts_load_dword %5, %8, 0x280\n\t"
+                 "s_load_dword %6, %8, 0x300\n\ts_load_dword %7, %8, 0x380\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(v0), "=&s"(v1), "=&s"(v2), "=&s"(v3), "=&s"(v4), "=&s"(v5), "=&s"(v6), "=&s"(v7)
+                 : "s"(p) : "memory");
+    return __uint_as_float(max(max(max(v0, v1), max(v2, v3)), max(max(v4, v5), max(v6, v7))));
+}
+
 __device__ __forceinline__ void pin_all(uint4 (&wd)[3][8][2], uint4 (&wr)[8][2]) {
 #pragma unroll
     for (int tp = 0; tp < 3; ++tp)
